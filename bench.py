@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Benchmark: alignment columns/s for forward + Viterbi on a synthetic 3-species + outgroup
+alignment (BASELINE.json config 2: 5 + 5 intervals -> N = 70 hidden states, 10 Mbp per GPU).
+
+One step = the whole decoding hot path over the batch already resident in HBM:
+  forward log-likelihood of every MAF block (optimizer.py:145-188) + the log-likelihood
+  exchange across ranks (RCCL all-reduce, N > 1) + Viterbi with traceback of every block
+  (optimizer.py:305-354).
+The HMM is the reference's own (5,5) model build (tests/golden/model_kat_5_5.npz, produced by
+trans_emiss_calc with the KAT parameters of SURVEY 8c); columns are sampled from it
+(itrails_amd/synth.py), geometric block lengths with mean 2 kbp.
+
+Contract: python bench.py --gpus N --steps K --warmup W ; for N > 1 launched by
+torch.distributed.run, one rank per GPU; rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 (vector = matrix rate), AMD spec
+
+
+def load_model(n_int: int):
+    f = os.path.join(ROOT, "tests", "golden", f"model_kat_{n_int}_{n_int}.npz")
+    if os.path.exists(f):
+        g = np.load(f)
+        return g["a"], g["b"], g["pi"], f"itrails ({n_int},{n_int}) KAT model"
+    # same state count, random HMM (only until the reference model fixture exists)
+    g = np.load(os.path.join(ROOT, "tests", "golden", "sweep_syn70.npz"))
+    return g["a"], g["b"], g["pi"], "random N=70 HMM (sweep_syn70 fixture)"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n-int", type=int, default=5)
+    ap.add_argument("--mbp", type=float, default=10.0, help="columns per GPU (Mbp)")
+    ap.add_argument("--mean-block", type=float, default=2000.0)
+    ap.add_argument("--cpu-sample", type=int, default=400_000,
+                    help="columns of the bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--check", action="store_true", help="verify against the CPU oracle")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from itrails_amd import hmm
+    from itrails_amd.synth import block_lengths, sample_alignment
+
+    a, b, pi, model_name = load_model(args.n_int)
+    n = a.shape[0]
+    cols = int(args.mbp * 1e6)
+    rng = np.random.default_rng(12345 + rank)
+    lengths = block_lengths(rng, cols, args.mean_block)
+    t0 = time.time()
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=777 + rank)
+    gen_s = time.time() - t0
+
+    model = hmm.Model(a, b, pi)
+    plan = hmm.Plan(off)
+    plan.reserve(n, posterior=False)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).to(dev)
+    d_ll = torch.empty(plan.nblocks, dtype=torch.float64, device=dev)
+    d_path = torch.empty(plan.total, dtype=torch.uint8, device=dev)
+    nblk_global = plan.nblocks
+    if world > 1:
+        counts = torch.tensor([plan.nblocks], device=dev)
+        allc = [torch.zeros_like(counts) for _ in range(world)]
+        dist.all_gather(allc, counts)
+        counts = [int(c.item()) for c in allc]
+        nblk_global = sum(counts)
+        first = sum(counts[:rank])
+        d_ll_global = torch.zeros(nblk_global, dtype=torch.float64, device=dev)
+
+    fwd_ms, vit_ms, tb_ms = [], [], []
+
+    def step(timing=False):
+        hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
+        if timing:
+            fwd_ms.append(hmm.last_kernel_ms("forward"))
+        if world > 1:
+            # each rank owns a disjoint slice of the global block vector: the all-reduce is
+            # an exact gather (x + 0 = x), and the host sums in block order
+            d_ll_global.zero_()
+            d_ll_global[first:first + plan.nblocks] = d_ll
+            dist.all_reduce(d_ll_global)
+        hmm.viterbi_device(model, plan, d_obs, out=d_path)
+        if timing:
+            vit_ms.append(hmm.last_kernel_ms("viterbi"))
+            tb_ms.append(hmm.last_kernel_ms("traceback"))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    # kernel durations (HIP events on the launch stream), separate instrumented passes
+    for _ in range(max(1, min(args.steps, 3))):
+        step(timing=True)
+        torch.cuda.synchronize()
+
+    total_cols = cols * world
+    value = total_cols * args.steps / dt
+    ll_total = None
+    ll_host = (d_ll_global if world > 1 else d_ll).cpu().numpy()
+    acc = 0.0
+    for v in ll_host.tolist():
+        acc += v
+    ll_total = acc
+
+    result = None
+    if rank == 0:
+        vit_avg = float(np.mean(vit_ms))
+        ops_per_col = 2.0 * n * n  # Viterbi: one add + one max per (i, j) pair
+        achieved = ops_per_col * cols / (vit_avg * 1e-3) / 1e12
+        cpu = None
+        if args.cpu_sample > 0:
+            cpu = cpu_baseline(a, b, pi, obs, off, args.cpu_sample)
+        check = None
+        if args.check:
+            check = verify(a, b, pi, obs, off, ll_host if world == 1 else d_ll.cpu().numpy(),
+                           d_path.cpu().numpy())
+        result = {
+            "metric": "alignment columns/s (forward+Viterbi), 3sp+outgroup HMM",
+            "value": round(value, 1),
+            "unit": "columns/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: columns sampled from the reference's (5,5) KAT model, "
+                    "geometric blocks mean 2 kbp, 1% gaps + 0.5% N",
+            "config": {"workload": f"{args.mbp:g} Mbp/GPU, {n_int_label(args.n_int)}, "
+                                   "forward loglik + Viterbi traceback",
+                       "model": model_name, "hidden_states": n,
+                       "columns_per_gpu": cols, "blocks_per_gpu": int(plan.nblocks),
+                       "longest_block": int(np.diff(off).max()),
+                       "parallelism": f"block-sharded x{world}"},
+            "roofline": {"kernel": "sweep_kernel<VIT> (Viterbi max-plus)",
+                         "bound": "mfma", "pipe": "FP64 VALU (add/max; FP64 vector rate = "
+                                                  "FP64 matrix rate on MI355X)",
+                         "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
+                         "traffic": None,
+                         "kernel_ms": round(vit_avg, 4),
+                         "forward_ms": round(float(np.mean(fwd_ms)), 4),
+                         "traceback_ms": round(float(np.mean(tb_ms)), 4),
+                         "algorithmic": f"{ops_per_col:.0f} FP64 ops/column x {cols} columns"},
+            "cpu_baseline": cpu,
+            "loglik_total": ll_total,
+            "gen_seconds": round(gen_s, 2),
+        }
+        if check is not None:
+            result["check"] = check
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def n_int_label(k):
+    return f"{k}+{k} intervals"
+
+
+def cpu_baseline(a, b, pi, obs, off, sample_cols):
+    """The repo's C restatement of the reference sweeps (oracle/, OpenMP over blocks),
+    forward + Viterbi on a bounded prefix of this rank's blocks."""
+    from itrails_amd.tables import build_tables
+    from oracle import hmm_oracle as O
+
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    os.environ["OMP_NUM_THREADS"] = str(cores)
+    nb = int(np.searchsorted(off, sample_cols))
+    nb = max(1, min(nb, len(off) - 1))
+    o2 = off[: nb + 1]
+    ob = obs[: o2[-1]]
+    t = build_tables(a, b, pi)
+    O.lib()
+    t0 = time.perf_counter()
+    O.forward_loglik(t, ob, o2)
+    O.viterbi(t, ob, o2)
+    dt = time.perf_counter() - t0
+    return {"value": round(float(o2[-1]) / dt, 1), "unit": "columns/s", "cores": cores,
+            "kind": "port",
+            "sample": f"first {nb} blocks ({int(o2[-1])} columns) of the same workload, "
+                      f"forward + Viterbi, {dt:.2f} s"}
+
+
+def verify(a, b, pi, obs, off, ll, path):
+    from itrails_amd.tables import build_tables
+    from oracle import hmm_oracle as O
+
+    nb = int(np.searchsorted(off, 300_000))
+    o2 = off[: nb + 1]
+    t = build_tables(a, b, pi)
+    ref_ll = O.forward_loglik(t, obs[: o2[-1]], o2)
+    ref_p = O.viterbi(t, obs[: o2[-1]], o2)
+    rel = float(np.max(np.abs(ll[:nb] - ref_ll) / np.abs(ref_ll)))
+    return {"blocks": nb, "loglik_max_rel_err": rel,
+            "viterbi_equal": bool((path[: o2[-1]] == ref_p).all())}
+
+
+if __name__ == "__main__":
+    main()

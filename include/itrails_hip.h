@@ -1,0 +1,140 @@
+/*
+ * itrails_hip.h — C ABI of the MI355X (gfx950) coalescent-HMM decoding core.
+ *
+ * The reference (trails-phylogeny/itrails) has no FFI: its hot path is a Python call layer.
+ * Every entry point below replaces one reference function; the host wrapper
+ * (itrails_amd/hmm.py, itrails_amd/model.py) keeps the reference signatures and calls these
+ * through ctypes.  Reference files are cited relative to /root/reference/src/itrails/.
+ *
+ * Conventions
+ *  - Plain C types only: pointers + sizes; no torch / HIP types in the signatures.
+ *  - `d_` pointers are DEVICE pointers (HBM-resident, e.g. torch.cuda tensors' data_ptr());
+ *    `h_` pointers are host pointers.  `stream` is a hipStream_t passed as void* (NULL =
+ *    the default stream of the current device).
+ *  - Every function returns 0 on success and a non-zero ITR_E* code on failure; the message
+ *    of the last failure on this thread is itr_last_error().  Nothing aborts the process.
+ *  - Device selection follows the HIP current device of the calling thread (one process per
+ *    GPU; multi-GPU sharding and the RCCL log-likelihood all-reduce live in the host layer,
+ *    itrails_amd/distributed.py).
+ *  - Observed columns are uint16 symbols 0..624 of the 625-letter alphabet of
+ *    read_data.py:6-24 (0..255 = A/C/T/G^4 in species order, 256..624 contain N).
+ *  - Hidden states: 1 <= N <= 192 (n_int up to 8+8; Viterbi back-pointers are uint8).
+ */
+#ifndef ITRAILS_HIP_H
+#define ITRAILS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ITR_API __attribute__((visibility("default")))
+
+#define ITR_OK 0
+#define ITR_EINVAL 1   /* bad argument (shape, range, null pointer)           */
+#define ITR_EHIP 2     /* HIP runtime error (allocation, launch, copy)         */
+#define ITR_ESTATE 3   /* object used in the wrong state                       */
+
+#define ITR_NOBS 625   /* observed alphabet size, read_data.py:6-24            */
+#define ITR_MAX_STATES 192
+
+typedef struct itr_model* itr_model_t; /* HMM tables resident on one device          */
+typedef struct itr_plan* itr_plan_t;   /* block layout of one alignment + workspace   */
+
+/* ---------------------------------------------------------------------------------- */
+/* library                                                                             */
+/* ---------------------------------------------------------------------------------- */
+ITR_API int itr_version(void);               /* ABI version, currently 1             */
+ITR_API const char* itr_last_error(void);    /* message of the last failure (thread) */
+ITR_API int itr_device_count(int* n);
+
+/* ---------------------------------------------------------------------------------- */
+/* model tables                                                                        */
+/*                                                                                     */
+/* Replaces the (a, b, pi, order) argument group of optimizer.py:145-377.  The host     */
+/* builds, with NumPy, exactly the per-column quantities the reference evaluates        */
+/* (bit parity for Viterbi):                                                            */
+/*   a        N x N      transition matrix (get_trans_emiss.py:166-168)                 */
+/*   log_a    N x N      np.log(a)                          (optimizer.py:328)          */
+/*   emit     625 x N    E[o] = b[:, order[o]].sum(axis=1)  (optimizer.py:182,186,329)  */
+/*   log_emit 625 x N    np.log(E[o])                       (optimizer.py:329)          */
+/*   pi_emit  625 x N    pi * E[o]                          (optimizer.py:182)          */
+/*   log_pi_emit 625xN   np.log(pi * E[o])                  (optimizer.py:182,323)      */
+/* all row-major float64 host arrays; they are copied to the current device.           */
+/* ---------------------------------------------------------------------------------- */
+ITR_API int itr_model_create(int n_states, const double* h_a, const double* h_log_a,
+                             const double* h_emit, const double* h_log_emit,
+                             const double* h_pi_emit, const double* h_log_pi_emit,
+                             itr_model_t* out);
+ITR_API int itr_model_destroy(itr_model_t model);
+ITR_API int itr_model_n_states(itr_model_t model, int* n);
+
+/* ---------------------------------------------------------------------------------- */
+/* plans                                                                               */
+/*                                                                                     */
+/* A plan describes one alignment as n_blocks MAF blocks laid out back to back:        */
+/* block k owns columns [h_block_off[k], h_block_off[k+1]) of the observation array    */
+/* (the V_lst list of read_data.py:94-117, concatenated).  Empty blocks are allowed.   */
+/* The plan uploads the offsets and a longest-first processing order and owns the      */
+/* device workspace (Viterbi back-pointers, forward rows for posteriors).              */
+/* ---------------------------------------------------------------------------------- */
+ITR_API int itr_plan_create(const int64_t* h_block_off, int64_t n_blocks, itr_plan_t* out);
+ITR_API int itr_plan_destroy(itr_plan_t plan);
+ITR_API int itr_plan_total_columns(itr_plan_t plan, int64_t* total);
+/* grow the workspace now (optional; the sweeps grow it on demand) */
+ITR_API int itr_plan_reserve(itr_plan_t plan, int n_states, int for_posterior);
+
+/* ---------------------------------------------------------------------------------- */
+/* sweeps over device-resident observations                                            */
+/* ---------------------------------------------------------------------------------- */
+
+/* Per-block forward log-likelihood.
+ * Replaces forward / forward_loglik (optimizer.py:145-188) for every block of the plan;
+ * d_loglik[k] = log P(block k).  The host sums d_loglik in block order, as
+ * loglik_wrapper does (optimizer.py:93-116). */
+ITR_API int itr_forward_loglik(itr_model_t model, itr_plan_t plan, const uint16_t* d_obs,
+                               double* d_loglik, void* stream);
+
+/* Most likely hidden path of every block.
+ * Replaces viterbi + backtrack_viterbi (optimizer.py:305-354) as called by viterbi_wrapper
+ * (optimizer.py:357-377): d_path[c] = state index at column c (uint8; the reference returns
+ * the same integers as float64).  Ties resolve to the lowest index, like np.argmax. */
+ITR_API int itr_viterbi(itr_model_t model, itr_plan_t plan, const uint16_t* d_obs,
+                        uint8_t* d_path, void* stream);
+
+/* Posterior decoding.
+ * Replaces post_prob (optimizer.py:216-238) including the reference's backward recursion
+ * beta_t = (beta_{t+1} * e_{t+1}) @ a (optimizer.py:207-212): d_post is (total_columns x N)
+ * row-major float64, each row summing to 1. */
+ITR_API int itr_posterior(itr_model_t model, itr_plan_t plan, const uint16_t* d_obs,
+                          double* d_post, void* stream);
+
+/* Host-buffer conveniences (synchronous; copy in, run, copy out). */
+ITR_API int itr_forward_loglik_host(itr_model_t model, itr_plan_t plan,
+                                    const uint16_t* h_obs, double* h_loglik);
+ITR_API int itr_viterbi_host(itr_model_t model, itr_plan_t plan, const uint16_t* h_obs,
+                             uint8_t* h_path);
+ITR_API int itr_posterior_host(itr_model_t model, itr_plan_t plan, const uint16_t* h_obs,
+                               double* h_post);
+
+/* Timing hook for benchmarks: average device duration (ms) of the dominant kernel of the
+ * last sweep issued on this thread, measured with HIP events on the sweep's stream. */
+ITR_API int itr_last_kernel_ms(const char* which, double* ms);
+
+/* ---------------------------------------------------------------------------------- */
+/* model build: batched matrix exponential                                             */
+/* ---------------------------------------------------------------------------------- */
+
+/* out[b] = expm(A[b]) for b < batch, each n x n row-major float64 (device pointers).
+ * Replaces expm (expm.py:9-167): Higham's Pade 3/5/7/9/13 with scaling & squaring, the
+ * branch chosen per matrix from its 1-norm exactly as expm.py:16-143. */
+ITR_API int itr_expm_batched(int n, int64_t batch, const double* d_A, double* d_out,
+                             void* stream);
+ITR_API int itr_expm_batched_host(int n, int64_t batch, const double* h_A, double* h_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ITRAILS_HIP_H */

@@ -1,0 +1,41 @@
+"""Build libitrails_hip.so in-tree with hipcc for gfx950 (no JIT cache, no torch extension:
+the library is a plain C-ABI shared object so it travels with the repository snapshot)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+SOURCES = ["hmm_sweeps.hip", "expm.hip", "capi.cpp"]
+OUT = os.path.join(HERE, "libitrails_hip.so")
+ARCH = os.environ.get("ITR_OFFLOAD_ARCH", "gfx950")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    deps.append(os.path.join(os.path.dirname(HERE), "include", "itrails_hip.h"))
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return OUT
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-fvisibility=hidden"]
+    cmd += [os.path.join(CSRC, s) for s in SOURCES]
+    cmd += ["-o", OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,510 @@
+// capi.cpp — the C ABI declared in include/itrails_hip.h: object lifetimes, argument
+// checking, workspace management and kernel launches.  No compute happens on the host.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/itrails_hip.h"
+#include "sweeps.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(ITR_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),         \
+                  __FILE__, __LINE__);                                                     \
+  } while (0)
+
+// ---- per-thread kernel timing (HIP events on the launch stream) -----------------------
+struct Timer {
+  std::string name;
+  int device = -1;
+  hipEvent_t a = nullptr, b = nullptr;
+  bool armed = false;
+};
+thread_local std::vector<Timer> g_timers;
+
+Timer* timer(const char* name) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  for (auto& t : g_timers)
+    if (t.name == name) {
+      if (t.device != dev) {
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+        t.a = t.b = nullptr;
+      }
+      if (!t.a) {
+        (void)hipEventCreate(&t.a);
+        (void)hipEventCreate(&t.b);
+        t.device = dev;
+      }
+      return &t;
+    }
+  g_timers.push_back(Timer{name, dev});
+  Timer* t = &g_timers.back();
+  (void)hipEventCreate(&t->a);
+  (void)hipEventCreate(&t->b);
+  return t;
+}
+struct Scope {
+  Timer* t;
+  hipStream_t s;
+  Scope(const char* name, hipStream_t st) : t(timer(name)), s(st) {
+    (void)hipEventRecord(t->a, s);
+  }
+  ~Scope() {
+    (void)hipEventRecord(t->b, s);
+    t->armed = true;
+  }
+};
+
+int cu_count() {
+  int dev = 0, n = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    n = 256;
+  return n > 0 ? n : 256;
+}
+
+template <class T>
+int dev_alloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
+  return 0;
+}
+template <class T>
+void dev_free(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+}  // namespace
+
+struct itr_model {
+  int device = 0;
+  int n = 0;
+  double *a = nullptr, *la = nullptr, *E = nullptr, *LE = nullptr, *PIE = nullptr,
+         *LPIE = nullptr;
+};
+
+struct itr_plan {
+  int device = 0;
+  int64_t nblocks = 0, total = 0, nchunks = 0;
+  int64_t *d_off = nullptr, *d_chunk_base = nullptr;
+  int32_t *d_order = nullptr, *d_chunk_blk = nullptr;
+  int* d_queue = nullptr;
+  // workspace (grown on demand)
+  uint8_t* d_bp = nullptr;
+  size_t bp_cap = 0;
+  uint8_t* d_chunk_map = nullptr;
+  size_t cm_cap = 0;
+  uint8_t* d_chunk_end = nullptr;
+  uint8_t* d_last = nullptr;
+  double* d_alpha = nullptr;
+  size_t alpha_cap = 0;
+};
+
+namespace {
+
+int check_model(itr_model_t m) {
+  if (!m) return fail(ITR_EINVAL, "null model");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (dev != m->device)
+    return fail(ITR_ESTATE, "model lives on device %d, current device is %d", m->device, dev);
+  return 0;
+}
+int check_plan(itr_plan_t p) {
+  if (!p) return fail(ITR_EINVAL, "null plan");
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (dev != p->device)
+    return fail(ITR_ESTATE, "plan lives on device %d, current device is %d", p->device, dev);
+  return 0;
+}
+
+int reserve(itr_plan_t p, int n, bool vit, bool post) {
+  if (vit) {
+    const size_t need = (size_t)p->total * n;
+    if (need > p->bp_cap) {
+      dev_free(p->d_bp);
+      if (int e = dev_alloc(&p->d_bp, need)) return e;
+      p->bp_cap = need;
+    }
+    const size_t needc = (size_t)p->nchunks * n;
+    if (needc > p->cm_cap) {
+      dev_free(p->d_chunk_map);
+      if (int e = dev_alloc(&p->d_chunk_map, needc)) return e;
+      p->cm_cap = needc;
+    }
+  }
+  if (post) {
+    const size_t need = (size_t)p->total * n;
+    if (need > p->alpha_cap) {
+      dev_free(p->d_alpha);
+      if (int e = dev_alloc(&p->d_alpha, need)) return e;
+      p->alpha_cap = need;
+    }
+  }
+  return 0;
+}
+
+itr::SweepArgs base_args(itr_model_t m, itr_plan_t p, const uint16_t* obs) {
+  itr::SweepArgs a{};
+  a.n = m->n;
+  a.nblocks = p->nblocks;
+  a.off = p->d_off;
+  a.order = p->d_order;
+  a.queue = p->d_queue;
+  a.obs = obs;
+  a.chunk_base = p->d_chunk_base;
+  return a;
+}
+
+int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname) {
+  itr::SweepGeometry g = itr::sweep_geometry(a.n, mode);
+  if (g.iq < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", a.n);
+  a.xp = g.xp;
+  int64_t grid = (int64_t)g.per_cu * cu_count();
+  if (grid > a.nblocks) grid = a.nblocks;
+  if (grid <= 0) return 0;
+  HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
+  {
+    Scope sc(tname, st);
+    HIP_TRY(itr::launch_sweep(mode, g, (int)grid, a, st));
+  }
+  return 0;
+}
+
+int g_force_slow = 0;  // test hook (environment ITR_FORCE_SLOW_TIES=1)
+
+}  // namespace
+
+extern "C" {
+
+int itr_version(void) { return 1; }
+
+const char* itr_last_error(void) { return g_err.c_str(); }
+
+int itr_device_count(int* n) {
+  if (!n) return fail(ITR_EINVAL, "null pointer");
+  HIP_TRY(hipGetDeviceCount(n));
+  return 0;
+}
+
+int itr_model_create(int n, const double* a, const double* la, const double* E,
+                     const double* LE, const double* PIE, const double* LPIE,
+                     itr_model_t* out) {
+  if (!out) return fail(ITR_EINVAL, "null output pointer");
+  *out = nullptr;
+  if (n < 1 || n > ITR_MAX_STATES)
+    return fail(ITR_EINVAL, "n_states=%d outside [1, %d]", n, ITR_MAX_STATES);
+  if (!a || !la || !E || !LE || !PIE || !LPIE) return fail(ITR_EINVAL, "null table pointer");
+  auto* m = new itr_model();
+  m->n = n;
+  if (hipGetDevice(&m->device) != hipSuccess) {
+    delete m;
+    return fail(ITR_EHIP, "hipGetDevice failed");
+  }
+  const size_t nn = (size_t)n * n, on = (size_t)ITR_NOBS * n;
+  double** dst[6] = {&m->a, &m->la, &m->E, &m->LE, &m->PIE, &m->LPIE};
+  const double* src[6] = {a, la, E, LE, PIE, LPIE};
+  const size_t cnt[6] = {nn, nn, on, on, on, on};
+  for (int i = 0; i < 6; ++i) {
+    int e = dev_alloc(dst[i], cnt[i]);
+    if (!e && hipMemcpy(*dst[i], src[i], cnt[i] * sizeof(double), hipMemcpyHostToDevice) !=
+                  hipSuccess)
+      e = fail(ITR_EHIP, "table upload failed");
+    if (e) {
+      itr_model_destroy(m);
+      return e;
+    }
+  }
+  *out = m;
+  return 0;
+}
+
+int itr_model_destroy(itr_model_t m) {
+  if (!m) return 0;
+  dev_free(m->a);
+  dev_free(m->la);
+  dev_free(m->E);
+  dev_free(m->LE);
+  dev_free(m->PIE);
+  dev_free(m->LPIE);
+  delete m;
+  return 0;
+}
+
+int itr_model_n_states(itr_model_t m, int* n) {
+  if (!m || !n) return fail(ITR_EINVAL, "null pointer");
+  *n = m->n;
+  return 0;
+}
+
+int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
+  if (!out) return fail(ITR_EINVAL, "null output pointer");
+  *out = nullptr;
+  if (nblocks < 0 || (nblocks > 0 && !off)) return fail(ITR_EINVAL, "bad block offsets");
+  if (nblocks > INT32_MAX) return fail(ITR_EINVAL, "too many blocks");
+  std::vector<int64_t> h_off(off, off + nblocks + 1);
+  if (h_off[0] != 0) return fail(ITR_EINVAL, "block_off[0] must be 0");
+  for (int64_t k = 0; k < nblocks; ++k) {
+    if (h_off[k + 1] < h_off[k]) return fail(ITR_EINVAL, "block offsets decrease at %lld",
+                                            (long long)k);
+    if (h_off[k + 1] - h_off[k] > INT32_MAX) return fail(ITR_EINVAL, "block too long");
+  }
+  auto* p = new itr_plan();
+  (void)hipGetDevice(&p->device);
+  p->nblocks = nblocks;
+  p->total = h_off[nblocks];
+  // longest-first processing order (stable: equal lengths keep block order)
+  std::vector<int32_t> order(nblocks);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
+    return h_off[x + 1] - h_off[x] > h_off[y + 1] - h_off[y];
+  });
+  // traceback chunks
+  std::vector<int64_t> cbase(nblocks);
+  std::vector<int32_t> cblk;
+  int64_t nc = 0;
+  for (int64_t k = 0; k < nblocks; ++k) {
+    cbase[k] = nc;
+    const int64_t T = h_off[k + 1] - h_off[k];
+    const int64_t K = (T + itr::VIT_CHUNK - 1) / itr::VIT_CHUNK;
+    for (int64_t c = 0; c < K; ++c) cblk.push_back((int32_t)k);
+    nc += K;
+  }
+  p->nchunks = nc;
+  int e = 0;
+  if (!e) e = dev_alloc(&p->d_off, nblocks + 1);
+  if (!e) e = dev_alloc(&p->d_order, nblocks);
+  if (!e) e = dev_alloc(&p->d_chunk_base, nblocks);
+  if (!e) e = dev_alloc(&p->d_chunk_blk, nc);
+  if (!e) e = dev_alloc(&p->d_queue, 4);
+  if (!e) e = dev_alloc(&p->d_chunk_end, nc);
+  if (!e) e = dev_alloc(&p->d_last, nblocks);
+  auto up = [&](void* d, const void* h, size_t bytes) {
+    if (e || bytes == 0) return;
+    if (hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) != hipSuccess)
+      e = fail(ITR_EHIP, "plan upload failed");
+  };
+  up(p->d_off, h_off.data(), (nblocks + 1) * sizeof(int64_t));
+  up(p->d_order, order.data(), nblocks * sizeof(int32_t));
+  up(p->d_chunk_base, cbase.data(), nblocks * sizeof(int64_t));
+  up(p->d_chunk_blk, cblk.data(), nc * sizeof(int32_t));
+  if (e) {
+    itr_plan_destroy(p);
+    return e;
+  }
+  const char* fs = getenv("ITR_FORCE_SLOW_TIES");
+  g_force_slow = (fs && fs[0] == '1') ? 1 : 0;
+  *out = p;
+  return 0;
+}
+
+int itr_plan_destroy(itr_plan_t p) {
+  if (!p) return 0;
+  dev_free(p->d_off);
+  dev_free(p->d_order);
+  dev_free(p->d_chunk_base);
+  dev_free(p->d_chunk_blk);
+  dev_free(p->d_queue);
+  dev_free(p->d_bp);
+  dev_free(p->d_chunk_map);
+  dev_free(p->d_chunk_end);
+  dev_free(p->d_last);
+  dev_free(p->d_alpha);
+  delete p;
+  return 0;
+}
+
+int itr_plan_total_columns(itr_plan_t p, int64_t* total) {
+  if (!p || !total) return fail(ITR_EINVAL, "null pointer");
+  *total = p->total;
+  return 0;
+}
+
+int itr_plan_reserve(itr_plan_t p, int n, int for_posterior) {
+  if (int e = check_plan(p)) return e;
+  if (n < 1 || n > ITR_MAX_STATES) return fail(ITR_EINVAL, "bad n_states");
+  return reserve(p, n, !for_posterior, for_posterior != 0);
+}
+
+int itr_forward_loglik(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* loglik,
+                       void* stream) {
+  if (int e = check_model(m)) return e;
+  if (int e = check_plan(p)) return e;
+  if (p->nblocks == 0) return 0;
+  if ((!obs && p->total > 0) || !loglik) return fail(ITR_EINVAL, "null device pointer");
+  hipStream_t st = (hipStream_t)stream;
+  itr::SweepArgs a = base_args(m, p, obs);
+  a.mat = m->a;
+  a.emit = m->E;
+  a.init = m->PIE;
+  a.loglik = loglik;
+  return run_sweep(itr::MODE_FWD_LL, a, st, "forward");
+}
+
+int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
+                void* stream) {
+  if (int e = check_model(m)) return e;
+  if (int e = check_plan(p)) return e;
+  if (p->nblocks == 0 || p->total == 0) return 0;
+  if (!obs || !path) return fail(ITR_EINVAL, "null device pointer");
+  if (int e = reserve(p, m->n, true, false)) return e;
+  hipStream_t st = (hipStream_t)stream;
+  itr::SweepArgs a = base_args(m, p, obs);
+  a.mat = m->la;
+  a.emit = m->LE;
+  a.init = m->LPIE;
+  a.bp = p->d_bp;
+  a.chunk_map = p->d_chunk_map;
+  a.last_state = p->d_last;
+  a.force_slow = g_force_slow;
+  if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
+  Scope sc("traceback", st);
+  HIP_TRY(itr::launch_vit_traceback(m->n, p->nblocks, p->nchunks, p->d_off, p->d_chunk_base,
+                                    p->d_chunk_blk, p->d_chunk_map, p->d_last, p->d_chunk_end,
+                                    p->d_bp, path, st));
+  return 0;
+}
+
+int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post,
+                  void* stream) {
+  if (int e = check_model(m)) return e;
+  if (int e = check_plan(p)) return e;
+  if (p->nblocks == 0 || p->total == 0) return 0;
+  if (!obs || !post) return fail(ITR_EINVAL, "null device pointer");
+  if (int e = reserve(p, m->n, false, true)) return e;
+  hipStream_t st = (hipStream_t)stream;
+  itr::SweepArgs a = base_args(m, p, obs);
+  a.mat = m->a;
+  a.emit = m->E;
+  a.init = m->PIE;
+  a.alpha = p->d_alpha;
+  if (int e = run_sweep(itr::MODE_FWD_STORE, a, st, "posterior_fwd")) return e;
+  a.post = post;
+  return run_sweep(itr::MODE_BWD, a, st, "posterior_bwd");
+}
+
+// ---- host conveniences -----------------------------------------------------------------
+namespace {
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+}  // namespace
+
+int itr_forward_loglik_host(itr_model_t m, itr_plan_t p, const uint16_t* h_obs,
+                            double* h_ll) {
+  if (int e = check_plan(p)) return e;
+  if (p->nblocks == 0) return 0;
+  if ((!h_obs && p->total) || !h_ll) return fail(ITR_EINVAL, "null host pointer");
+  DevBuf o, l;
+  HIP_TRY(hipMalloc(&o.p, std::max<int64_t>(p->total, 1) * sizeof(uint16_t)));
+  HIP_TRY(hipMalloc(&l.p, p->nblocks * sizeof(double)));
+  if (p->total)
+    HIP_TRY(hipMemcpy(o.p, h_obs, p->total * sizeof(uint16_t), hipMemcpyHostToDevice));
+  if (int e = itr_forward_loglik(m, p, (const uint16_t*)o.p, (double*)l.p, nullptr)) return e;
+  HIP_TRY(hipMemcpy(h_ll, l.p, p->nblocks * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int itr_viterbi_host(itr_model_t m, itr_plan_t p, const uint16_t* h_obs, uint8_t* h_path) {
+  if (int e = check_plan(p)) return e;
+  if (p->total == 0) return 0;
+  if (!h_obs || !h_path) return fail(ITR_EINVAL, "null host pointer");
+  DevBuf o, y;
+  HIP_TRY(hipMalloc(&o.p, p->total * sizeof(uint16_t)));
+  HIP_TRY(hipMalloc(&y.p, p->total));
+  HIP_TRY(hipMemcpy(o.p, h_obs, p->total * sizeof(uint16_t), hipMemcpyHostToDevice));
+  if (int e = itr_viterbi(m, p, (const uint16_t*)o.p, (uint8_t*)y.p, nullptr)) return e;
+  HIP_TRY(hipMemcpy(h_path, y.p, p->total, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int itr_posterior_host(itr_model_t m, itr_plan_t p, const uint16_t* h_obs, double* h_post) {
+  if (int e = check_model(m)) return e;
+  if (int e = check_plan(p)) return e;
+  if (p->total == 0) return 0;
+  if (!h_obs || !h_post) return fail(ITR_EINVAL, "null host pointer");
+  DevBuf o, y;
+  const size_t bytes = (size_t)p->total * m->n * sizeof(double);
+  HIP_TRY(hipMalloc(&o.p, p->total * sizeof(uint16_t)));
+  HIP_TRY(hipMalloc(&y.p, bytes));
+  HIP_TRY(hipMemcpy(o.p, h_obs, p->total * sizeof(uint16_t), hipMemcpyHostToDevice));
+  if (int e = itr_posterior(m, p, (const uint16_t*)o.p, (double*)y.p, nullptr)) return e;
+  HIP_TRY(hipMemcpy(h_post, y.p, bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int itr_last_kernel_ms(const char* which, double* ms) {
+  if (!which || !ms) return fail(ITR_EINVAL, "null pointer");
+  for (auto& t : g_timers)
+    if (t.name == which && t.armed) {
+      HIP_TRY(hipEventSynchronize(t.b));
+      float f = 0.f;
+      HIP_TRY(hipEventElapsedTime(&f, t.a, t.b));
+      *ms = f;
+      return 0;
+    }
+  return fail(ITR_ESTATE, "no timing recorded for '%s'", which);
+}
+
+int itr_expm_batched(int n, int64_t batch, const double* A, double* out, void* stream) {
+  if (n < 1 || batch < 0) return fail(ITR_EINVAL, "bad expm shape n=%d batch=%lld", n,
+                                      (long long)batch);
+  if (batch == 0) return 0;
+  if (!A || !out) return fail(ITR_EINVAL, "null device pointer");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t wb = itr::expm_workspace_bytes(n, batch);
+  DevBuf w;
+  HIP_TRY(hipMallocAsync(&w.p, wb ? wb : 8, st));
+  Scope sc("expm", st);
+  hipError_t e = itr::launch_expm_batched(n, batch, A, out, (double*)w.p, st);
+  (void)hipFreeAsync(w.p, st);
+  w.p = nullptr;
+  if (e != hipSuccess) return fail(ITR_EHIP, "expm launch failed: %s", hipGetErrorString(e));
+  return 0;
+}
+
+int itr_expm_batched_host(int n, int64_t batch, const double* h_A, double* h_out) {
+  if (n < 1 || batch < 0) return fail(ITR_EINVAL, "bad expm shape");
+  if (batch == 0) return 0;
+  if (!h_A || !h_out) return fail(ITR_EINVAL, "null host pointer");
+  const size_t bytes = (size_t)batch * n * n * sizeof(double);
+  DevBuf a, o;
+  HIP_TRY(hipMalloc(&a.p, bytes));
+  HIP_TRY(hipMalloc(&o.p, bytes));
+  HIP_TRY(hipMemcpy(a.p, h_A, bytes, hipMemcpyHostToDevice));
+  if (int e = itr_expm_batched(n, batch, (const double*)a.p, (double*)o.p, nullptr)) return e;
+  HIP_TRY(hipMemcpy(h_out, o.p, bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+}  // extern "C"

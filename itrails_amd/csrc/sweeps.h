@@ -1,0 +1,57 @@
+// sweeps.h — internal interface between the C ABI (capi.cpp) and the HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace itr {
+
+enum SweepMode { MODE_FWD_LL = 0, MODE_FWD_STORE = 1, MODE_BWD = 2, MODE_VIT = 3 };
+
+// columns per Viterbi traceback chunk (bounds every pointer chase)
+static constexpr int VIT_CHUNK = 256;
+
+struct SweepArgs {
+  int n;                        // hidden states
+  int xp;                       // padded length of the LDS state vectors
+  int64_t nblocks;
+  const int64_t* off;           // [nblocks+1] column offsets of the blocks
+  const int32_t* order;         // [nblocks] processing order (longest first)
+  int* queue;                   // work counter, zero at launch
+  const uint16_t* obs;          // [total] observed symbols
+  const double* mat;            // a (forward/backward) or log a (Viterbi), n x n
+  const double* emit;           // E or log E, 625 x n
+  const double* init;           // pi*E or log(pi*E), 625 x n
+  double* loglik;               // [nblocks]                       (MODE_FWD_LL)
+  double* alpha;                // [total x n] rescaled forward rows (FWD_STORE out, BWD in)
+  double* post;                 // [total x n] posteriors          (MODE_BWD)
+  uint8_t* bp;                  // [total x n] back-pointers       (MODE_VIT)
+  uint8_t* chunk_map;           // [nchunks x n] chunk origin maps (MODE_VIT)
+  const int64_t* chunk_base;    // [nblocks] first chunk of each block
+  uint8_t* last_state;          // [nblocks] argmax of the last column (MODE_VIT)
+  int force_slow;               // test hook: take the Viterbi tie re-scan for every state
+};
+
+struct SweepGeometry {
+  int iq;       // source states per lane (template)
+  int block;    // threads per workgroup (64 * waves)
+  int xp;       // padded vector length
+  size_t lds;   // dynamic LDS bytes
+  int per_cu;   // resident workgroups per CU (occupancy API)
+};
+
+SweepGeometry sweep_geometry(int n, int mode);
+hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepArgs& a,
+                        hipStream_t st);
+hipError_t launch_vit_traceback(int n, int64_t nblocks, int64_t nchunks, const int64_t* off,
+                                const int64_t* chunk_base, const int32_t* chunk_blk,
+                                const uint8_t* chunk_map, const uint8_t* last_state,
+                                uint8_t* chunk_end, const uint8_t* bp, uint8_t* path,
+                                hipStream_t st);
+
+// batched matrix exponential (expm.hip)
+hipError_t launch_expm_batched(int n, int64_t batch, const double* A, double* out,
+                               double* work, hipStream_t st);
+size_t expm_workspace_bytes(int n, int64_t batch);
+
+}  // namespace itr

@@ -1,0 +1,235 @@
+"""HMM sweeps on the GPU behind the reference's own call surface.
+
+Two layers:
+
+* Device layer (`Model`, `Plan`, `forward_loglik_device`, `viterbi_device`,
+  `posterior_device`): inputs and outputs are torch.cuda tensors already resident in HBM;
+  every call is one C-ABI call (include/itrails_hip.h) on the current torch stream.
+* Reference layer — the functions of optimizer.py:145-377 with the same names, arguments,
+  return types and semantics (`forward_loglik`, `loglik_wrapper`, `loglik_wrapper_par`,
+  `viterbi_wrapper`, `post_prob`, `post_prob_wrapper`, `backtrack`-free `viterbi`), so a
+  caller written against the reference drops in unchanged.  `order` arguments are accepted
+  and ignored: the alphabet expansion is tabulated once (itrails_amd/tables.py).
+
+No code path here computes on the host: if libitrails_hip.so is missing or the device is
+unavailable the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, List, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr
+from .tables import HmmTables, build_tables
+
+__all__ = [
+    "Model", "Plan", "concat_blocks", "forward_loglik_device", "viterbi_device",
+    "posterior_device", "forward_loglik", "loglik_wrapper", "loglik_wrapper_par",
+    "viterbi_wrapper", "post_prob", "post_prob_wrapper", "block_logliks",
+]
+
+
+# ---------------------------------------------------------------------------------------
+# objects
+# ---------------------------------------------------------------------------------------
+class Model:
+    """Model tables resident on the current HIP device (itr_model_create)."""
+
+    def __init__(self, a=None, b=None, pi=None, tables: HmmTables | None = None):
+        self.tables = tables if tables is not None else build_tables(a, b, pi)
+        t = self.tables
+        if not 1 <= t.n <= _lib.MAX_STATES:
+            raise ValueError(f"{t.n} hidden states; the device path supports 1..{_lib.MAX_STATES}")
+        h = ctypes.c_void_p()
+        check(lib().itr_model_create(t.n, ptr(t.a), ptr(t.log_a), ptr(t.emit), ptr(t.log_emit),
+                                     ptr(t.pi_emit), ptr(t.log_pi_emit), ctypes.byref(h)))
+        self.handle = h.value
+        self.n = t.n
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().itr_model_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def concat_blocks(V_lst: Sequence[np.ndarray]):
+    """V_lst (list of int arrays of symbols, read_data.py:94-117) -> (uint16 obs, int64 off).
+
+    Symbols must be in [0, 625); the reference would raise IndexError on anything else."""
+    lens = np.fromiter((len(v) for v in V_lst), dtype=np.int64, count=len(V_lst))
+    off = np.zeros(len(V_lst) + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    if off[-1]:
+        obs = np.concatenate([np.asarray(v) for v in V_lst])
+        if obs.min() < 0 or obs.max() >= _lib.NOBS:
+            raise IndexError("observed symbol outside the 625-letter alphabet")
+        obs = obs.astype(np.uint16)
+    else:
+        obs = np.zeros(0, dtype=np.uint16)
+    return obs, off
+
+
+class Plan:
+    """Block layout of one alignment on the current device (itr_plan_create)."""
+
+    def __init__(self, block_off):
+        off = np.ascontiguousarray(block_off, dtype=np.int64)
+        if off.ndim != 1 or len(off) < 1 or off[0] != 0 or np.any(np.diff(off) < 0):
+            raise ValueError("block offsets must start at 0 and be non-decreasing")
+        self.off = off
+        self.nblocks = len(off) - 1
+        self.total = int(off[-1])
+        h = ctypes.c_void_p()
+        check(lib().itr_plan_create(ptr(off), self.nblocks, ctypes.byref(h)))
+        self.handle = h.value
+
+    def reserve(self, n: int, posterior: bool = False):
+        check(lib().itr_plan_reserve(self.handle, n, int(posterior)))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().itr_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _stream_handle():
+    import torch
+
+    return torch.cuda.current_stream().cuda_stream
+
+
+# ---------------------------------------------------------------------------------------
+# device layer (torch.cuda tensors)
+# ---------------------------------------------------------------------------------------
+def forward_loglik_device(model: Model, plan: Plan, d_obs, out=None):
+    """Per-block log-likelihoods (float64 [nblocks]) for int16/uint16 symbols on device."""
+    import torch
+
+    if out is None:
+        out = torch.empty(plan.nblocks, dtype=torch.float64, device=d_obs.device)
+    check(lib().itr_forward_loglik(model.handle, plan.handle, ptr(d_obs), ptr(out),
+                                   _stream_handle()))
+    return out
+
+
+def viterbi_device(model: Model, plan: Plan, d_obs, out=None):
+    """Viterbi state per column (uint8 [total])."""
+    import torch
+
+    if out is None:
+        out = torch.empty(plan.total, dtype=torch.uint8, device=d_obs.device)
+    check(lib().itr_viterbi(model.handle, plan.handle, ptr(d_obs), ptr(out), _stream_handle()))
+    return out
+
+
+def posterior_device(model: Model, plan: Plan, d_obs, out=None):
+    """Posterior state probabilities (float64 [total, N])."""
+    import torch
+
+    if out is None:
+        out = torch.empty((plan.total, model.n), dtype=torch.float64, device=d_obs.device)
+    check(lib().itr_posterior(model.handle, plan.handle, ptr(d_obs), ptr(out),
+                              _stream_handle()))
+    return out
+
+
+def last_kernel_ms(which: str) -> float:
+    v = ctypes.c_double()
+    check(lib().itr_last_kernel_ms(which.encode(), ctypes.byref(v)))
+    return v.value
+
+
+# ---------------------------------------------------------------------------------------
+# host-buffer helpers (copy in / run / copy out inside the library)
+# ---------------------------------------------------------------------------------------
+def block_logliks(model: Model, plan: Plan, obs: np.ndarray) -> np.ndarray:
+    out = np.zeros(plan.nblocks)
+    obs = np.ascontiguousarray(obs, dtype=np.uint16)
+    check(lib().itr_forward_loglik_host(model.handle, plan.handle, ptr(obs), ptr(out)))
+    return out
+
+
+def _paths(model: Model, plan: Plan, obs: np.ndarray) -> np.ndarray:
+    out = np.zeros(plan.total, dtype=np.uint8)
+    obs = np.ascontiguousarray(obs, dtype=np.uint16)
+    check(lib().itr_viterbi_host(model.handle, plan.handle, ptr(obs), ptr(out)))
+    return out
+
+
+def _posteriors(model: Model, plan: Plan, obs: np.ndarray) -> np.ndarray:
+    out = np.zeros((plan.total, model.n))
+    obs = np.ascontiguousarray(obs, dtype=np.uint16)
+    check(lib().itr_posterior_host(model.handle, plan.handle, ptr(obs), ptr(out)))
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# reference layer: optimizer.py:145-377
+# ---------------------------------------------------------------------------------------
+def loglik_wrapper(a, b, pi, V_lst: Iterable[np.ndarray]) -> float:
+    """Sum of forward log-likelihoods over blocks, accumulated in block order like
+    optimizer.py:93-116 (`acc += forward_loglik(...)`)."""
+    V_lst = list(V_lst)
+    if not V_lst:
+        return 0
+    obs, off = concat_blocks(V_lst)
+    model, plan = Model(a, b, pi), Plan(off)
+    ll = block_logliks(model, plan, obs)
+    acc = 0
+    for v in ll.tolist():
+        acc += v
+    return acc
+
+
+# optimizer.py:40-65 fans blocks out over joblib workers and sums in block order; on the
+# device all blocks of a process already run in parallel, and multi-GPU sharding is
+# itrails_amd.distributed.loglik_wrapper_dist.
+loglik_wrapper_par = loglik_wrapper
+
+
+def forward_loglik(a, b, pi, V, order=None) -> float:
+    """Log-likelihood of one block (optimizer.py:145-162)."""
+    return loglik_wrapper(a, b, pi, [V])
+
+
+def viterbi_wrapper(a, b, pi, V_lst: Iterable[np.ndarray]) -> List[np.ndarray]:
+    """Viterbi path per block as float64 arrays (optimizer.py:357-377, 336-354)."""
+    V_lst = list(V_lst)
+    obs, off = concat_blocks(V_lst)
+    if off[-1] == 0:
+        return [np.zeros(0) for _ in V_lst]
+    model, plan = Model(a, b, pi), Plan(off)
+    path = _paths(model, plan, obs).astype(np.float64)
+    return [path[off[k]:off[k + 1]] for k in range(len(V_lst))]
+
+
+def post_prob_wrapper(a, b, pi, V_lst: Iterable[np.ndarray]) -> List[np.ndarray]:
+    """Posterior matrices (T x N float64) per block (optimizer.py:241-262, 216-238)."""
+    V_lst = list(V_lst)
+    obs, off = concat_blocks(V_lst)
+    n = np.asarray(a).shape[0]
+    if off[-1] == 0:
+        return [np.zeros((0, n)) for _ in V_lst]
+    model, plan = Model(a, b, pi), Plan(off)
+    post = _posteriors(model, plan, obs)
+    return [post[off[k]:off[k + 1]] for k in range(len(V_lst))]
+
+
+def post_prob(a, b, pi, V, order=None) -> np.ndarray:
+    """Posterior matrix of one block (optimizer.py:216-238)."""
+    return post_prob_wrapper(a, b, pi, [V])[0]

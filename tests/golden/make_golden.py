@@ -1,0 +1,269 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the READ-ONLY reference.
+
+Runs only in the build container (the reference does not exist on the GPU box).  The
+reference is pure Python + numba; numba/Biopython are not installed here, so it is imported
+under the stand-in package in tests/golden/_shim (identity decorators, dict/list containers).
+Under the shim the reference runs as plain CPython + NumPy: `viterbi` and the model build
+are not numba-compiled in the reference either (optimizer.py:305, vanloan.py:392), so those
+outputs are the reference's own semantics; `forward`/`backward` lose numba's compilation but
+keep their arithmetic (optimizer.py:165-213).
+
+Fixtures are DATA only (inputs + expected outputs), written as .npz:
+
+  alphabet.npz          625 observed symbols and the `order` expansion table
+                        (read_data.py:6-24, 46-67)
+  model_<tag>.npz       a, b, pi, hidden state tuples from trans_emiss_calc
+                        (get_trans_emiss.py:8-170) for a parameter set
+  sweep_<tag>.npz       an HMM (a, b, pi), seeded blocks of observed symbols and the
+                        reference's forward_loglik / viterbi+backtrack_viterbi / post_prob
+                        outputs (optimizer.py:145-354)
+  expm_kat.npz          reference expm (expm.py:9-167) on matrices hitting every Pade branch
+
+Usage:  python tests/golden/make_golden.py alphabet|sweeps|expm|model <tag> ...
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF_SRC = "/root/reference/src"
+
+
+def _import_reference():
+    sys.path.insert(0, os.path.join(HERE, "_shim"))
+    sys.path.insert(0, REF_SRC)
+    import itrails.ncpu as ncpu
+
+    ncpu.update_n_cpu(1)
+    return ncpu
+
+
+# --------------------------------------------------------------------------------------
+# parameter sets (user units, like example_config.yaml); scaled exactly as
+# optimizer.py:396-557 does for the {t_1} case before calling trans_emiss_calc
+# --------------------------------------------------------------------------------------
+PARAMS = {
+    # the KAT set recorded in SURVEY.md 8(c)
+    "kat": dict(mu=2e-8, N_AB=50000.0, N_ABC=50000.0, t_1=240000.0, t_2=40000.0,
+                t_upper=745069.3855, r=1e-8),
+    # a second, asymmetric set: different Ne, faster recombination
+    "alt": dict(mu=1.5e-8, N_AB=30000.0, N_ABC=70000.0, t_1=180000.0, t_2=60000.0,
+                t_upper=500000.0, r=2.5e-8),
+}
+
+MODELS = {
+    # tag: (param set, n_int_AB, n_int_ABC)
+    "kat_1_1": ("kat", 1, 1),
+    "kat_2_2": ("kat", 2, 2),
+    "kat_3_3": ("kat", 3, 3),
+    "alt_2_3": ("alt", 2, 3),
+    "alt_3_2": ("alt", 3, 2),
+    "kat_4_4": ("kat", 4, 4),
+    "kat_5_5": ("kat", 5, 5),
+}
+
+
+def scaled_args(pset, n_ab, n_abc):
+    from itrails.cutpoints import cutpoints_ABC
+
+    p = PARAMS[pset]
+    mu = p["mu"]
+    t_1 = p["t_1"] * mu
+    t_2 = p["t_2"] * mu
+    t_upper = p["t_upper"] * mu
+    N_AB = p["N_AB"] * mu
+    N_ABC = p["N_ABC"] * mu
+    r = p["r"] / mu
+    cut_ABC = cutpoints_ABC(n_abc, 1)
+    t_A = t_B = t_1
+    t_C = t_1 + t_2
+    t_out = t_1 + t_2 + cut_ABC[n_abc - 1] * N_ABC + t_upper + 2 * N_ABC
+    return dict(t_A=t_A, t_B=t_B, t_C=t_C, t_2=t_2, t_upper=t_upper, t_out=t_out,
+                N_AB=N_AB, N_ABC=N_ABC, r=r, n_int_AB=n_ab, n_int_ABC=n_abc)
+
+
+def cmd_alphabet():
+    _import_reference()
+    from itrails.read_data import get_idx_state, get_obs_state_dct
+
+    names = get_obs_state_dct()
+    order = [np.asarray(get_idx_state(i), dtype=np.int64) for i in range(625)]
+    off = np.zeros(626, dtype=np.int64)
+    off[1:] = np.cumsum([len(o) for o in order])
+    np.savez_compressed(
+        os.path.join(HERE, "alphabet.npz"),
+        names=np.array(names),
+        order_flat=np.concatenate(order),
+        order_off=off,
+    )
+    print("alphabet.npz written")
+
+
+def cmd_model(tag):
+    _import_reference()
+    from itrails.get_trans_emiss import trans_emiss_calc
+
+    pset, n_ab, n_abc = MODELS[tag]
+    kw = scaled_args(pset, n_ab, n_abc)
+    t0 = time.time()
+    a, b, pi, hidden, observed = trans_emiss_calc(
+        kw["t_A"], kw["t_B"], kw["t_C"], kw["t_2"], kw["t_upper"], kw["t_out"],
+        kw["N_AB"], kw["N_ABC"], kw["r"], kw["n_int_AB"], kw["n_int_ABC"],
+        "standard", "standard")
+    dt = time.time() - t0
+    hidden_arr = np.array([hidden[i] for i in range(len(hidden))], dtype=np.int64)
+    obs_names = np.array([observed[i] for i in range(len(observed))])
+    np.savez_compressed(
+        os.path.join(HERE, f"model_{tag}.npz"),
+        a=a, b=b, pi=pi, hidden=hidden_arr, observed=obs_names,
+        args=np.array([kw[k] for k in ("t_A", "t_B", "t_C", "t_2", "t_upper", "t_out",
+                                       "N_AB", "N_ABC", "r")]),
+        n_int=np.array([n_ab, n_abc]), build_seconds=np.array(dt),
+    )
+    print(f"model_{tag}.npz written: N={a.shape[0]} in {dt:.1f}s")
+
+
+# --------------------------------------------------------------------------------------
+# sweeps
+# --------------------------------------------------------------------------------------
+def synthetic_hmm(rng, n, stay=(0.93, 0.995), sharp=0.3):
+    """Random HMM with a strong diagonal and distinct per-state emissions, so that the
+    Viterbi path switches states often (the reference models barely switch)."""
+    a = rng.random((n, n)) ** 3
+    np.fill_diagonal(a, 0.0)
+    a /= a.sum(1, keepdims=True)
+    d = rng.uniform(*stay, size=n)
+    a = a * (1 - d)[:, None]
+    a[np.arange(n), np.arange(n)] = d
+    b = rng.dirichlet(np.full(256, sharp), size=n)
+    pi = rng.dirichlet(np.ones(n))
+    return a, b, pi
+
+
+def sample_blocks(rng, a, b, pi, lengths, names, p_n=0.02, p_gap=0.01):
+    """Sample hidden paths from a and 4-species columns from b; inject N and '-' (-> N,
+    read_data.py:106) at the given rates.  Returns concatenated obs indices + offsets."""
+    n = a.shape[0]
+    index = {s: i for i, s in enumerate(names)}
+    letters = np.array(list("ACTG"))
+    obs = []
+    for T in lengths:
+        s = rng.choice(n, p=pi / pi.sum())
+        for t in range(T):
+            if t:
+                s = rng.choice(n, p=a[s])
+            c = rng.choice(256, p=b[s] / b[s].sum())
+            col = [letters[(c >> (2 * (3 - k))) & 3] for k in range(4)]
+            for k in range(4):
+                u = rng.random()
+                if u < p_n + p_gap:
+                    col[k] = "N"
+            obs.append(index["".join(col)])
+    off = np.zeros(len(lengths) + 1, dtype=np.int64)
+    off[1:] = np.cumsum(lengths)
+    return np.array(obs, dtype=np.uint16), off
+
+
+def run_reference_sweeps(a, b, pi, obs, off, post_rows_every):
+    from itrails.optimizer import backtrack_viterbi, forward_loglik, post_prob, viterbi
+    from itrails.read_data import get_idx_state
+
+    order = [get_idx_state(i) for i in range(625)]
+    ll, paths, post_idx, post_val = [], [], [], []
+    for k in range(len(off) - 1):
+        V = obs[off[k]:off[k + 1]].astype(np.int64)
+        ll.append(forward_loglik(a, b, pi, V, order))
+        om, prev = viterbi(a, b, pi, V, order)
+        paths.append(backtrack_viterbi(om, prev))
+        pp = post_prob(a, b, pi, V, order)
+        rows = np.unique(np.r_[0, np.arange(0, len(V), post_rows_every), len(V) - 1])
+        post_idx.append(rows + off[k])
+        post_val.append(pp[rows])
+    return (np.array(ll), np.concatenate(paths), np.concatenate(post_idx),
+            np.concatenate(post_val))
+
+
+def cmd_sweeps(only=()):
+    _import_reference()
+    from itrails.read_data import get_obs_state_dct
+
+    names = get_obs_state_dct()
+    cases = []
+    rng = np.random.default_rng(20260115)
+    # synthetic HMMs: small, odd, around a wavefront, and the two BASELINE sizes
+    for n, lengths in [
+        (4, [1, 2, 3, 50, 700]),
+        (13, [5, 1, 400, 1300]),
+        (27, [1, 64, 900, 2000]),
+        (65, [2, 300, 1700]),
+        (70, [1, 33, 1500, 2500]),
+        (133, [7, 600, 1400]),
+    ]:
+        a, b, pi = synthetic_hmm(rng, n)
+        cases.append((f"syn{n}", a, b, pi, lengths))
+    # real models from the reference model build (fixtures produced by `model`)
+    for tag, lengths in [("kat_3_3", [1, 5, 3000, 4000]), ("kat_5_5", [2, 2500, 3500])]:
+        f = os.path.join(HERE, f"model_{tag}.npz")
+        if not os.path.exists(f):
+            print("skip", tag, "(model fixture missing)")
+            continue
+        m = np.load(f)
+        cases.append((tag, m["a"], m["b"], m["pi"], lengths))
+    for tag, a, b, pi, lengths in cases:
+        t0 = time.time()
+        # every case draws from its own stream so a subset can be regenerated alone
+        rng = np.random.default_rng([20260115, sum(map(ord, tag))])
+        obs, off = sample_blocks(rng, a, b, pi, lengths, names)
+        if only and tag not in only:
+            continue
+        ll, path, pidx, pval = run_reference_sweeps(a, b, pi, obs, off, post_rows_every=37)
+        np.savez_compressed(
+            os.path.join(HERE, f"sweep_{tag}.npz"),
+            a=a, b=b, pi=pi, obs=obs, off=off, loglik=ll,
+            path=path.astype(np.int16), post_rows=pidx, post=pval)
+        switches = int((np.diff(path) != 0).sum())
+        print(f"sweep_{tag}.npz: N={a.shape[0]} cols={off[-1]} switches={switches} "
+              f"{time.time() - t0:.1f}s")
+
+
+def cmd_expm():
+    _import_reference()
+    from itrails.expm import expm
+
+    rng = np.random.default_rng(7)
+    out = {}
+    # 1-norms around every branch threshold of expm.py:16-140
+    # (theta = 1.5e-2, 2.5e-1, 9.5e-1, 2.1, 5.4; beyond -> scaling & squaring)
+    targets = (1e-3, 1.4e-2, 0.2, 0.9, 2.0, 5.0, 9.0, 40.0, 300.0)
+    for n in (2, 4, 15, 31, 203):
+        mats, outs = [], []
+        for target in (targets if n < 100 else targets[3::3]):
+            q = rng.random((n, n))
+            np.fill_diagonal(q, 0.0)
+            np.fill_diagonal(q, -q.sum(1))  # a rate matrix, like trans_mat.py:487-508
+            q *= target / np.abs(q).sum(0).max()
+            mats.append(q.copy())
+            outs.append(expm(q.copy()))
+        out[f"A_{n}"] = np.array(mats)
+        out[f"E_{n}"] = np.array(outs)
+    out["targets"] = np.array(targets)
+    np.savez_compressed(os.path.join(HERE, "expm_kat.npz"), **out)
+    print("expm_kat.npz written")
+
+
+if __name__ == "__main__":
+    cmd = sys.argv[1]
+    if cmd == "alphabet":
+        cmd_alphabet()
+    elif cmd == "model":
+        for t in sys.argv[2:]:
+            cmd_model(t)
+    elif cmd == "sweeps":
+        cmd_sweeps(tuple(sys.argv[2:]))
+    elif cmd == "expm":
+        cmd_expm()
+    else:
+        raise SystemExit(__doc__)

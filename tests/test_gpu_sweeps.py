@@ -1,0 +1,152 @@
+"""Device sweeps vs the reference (golden vectors) and vs the CPU oracle (larger inputs).
+
+Bars (BASELINE.json north_star): Viterbi paths identical (integer-exact); log-likelihoods
+and posteriors within 1e-8 relative.  Posteriors are compared with rtol=1e-8 and
+atol=1e-300 (values below ~1e-300 are denormal/underflowed in both computations).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden, model_fixtures, sweep_fixtures
+from itrails_amd import hmm
+from itrails_amd.synth import sample_alignment
+from itrails_amd.tables import build_tables
+from oracle import hmm_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-8
+
+
+def run_all(a, b, pi, obs, off):
+    model = hmm.Model(a, b, pi)
+    plan = hmm.Plan(off)
+    ll = hmm.block_logliks(model, plan, obs)
+    path = hmm._paths(model, plan, obs)
+    post = hmm._posteriors(model, plan, obs)
+    return ll, path, post
+
+
+def random_hmm(rng, n, stay=(0.9, 0.999)):
+    if n == 1:
+        return np.ones((1, 1)), rng.dirichlet(np.full(256, 0.3), size=1), np.ones(1)
+    a = rng.random((n, n)) ** 3
+    np.fill_diagonal(a, 0)
+    a /= a.sum(1, keepdims=True)
+    d = rng.uniform(*stay, size=n)
+    a = a * (1 - d)[:, None]
+    a[np.arange(n), np.arange(n)] = d
+    b = rng.dirichlet(np.full(256, 0.3), size=n)
+    pi = rng.dirichlet(np.ones(n))
+    return a, b, pi
+
+
+EDGE_LENGTHS = [1, 0, 2, 3, 255, 256, 257, 511, 512, 513, 17, 1000, 0, 4096, 1]
+
+
+@pytest.mark.parametrize("name", sweep_fixtures())
+def test_golden_sweeps(gpu, name):
+    g = golden(name)
+    ll, path, post = run_all(g["a"], g["b"], g["pi"], g["obs"], g["off"])
+    np.testing.assert_allclose(ll, g["loglik"], rtol=RTOL, atol=0)
+    np.testing.assert_array_equal(path, g["path"])
+    np.testing.assert_allclose(post[g["post_rows"]], g["post"], rtol=RTOL, atol=1e-300)
+
+
+@pytest.mark.parametrize("n", [1, 4, 16, 17, 27, 64, 70, 96, 133, 150, 192])
+def test_random_vs_oracle(gpu, n):
+    rng = np.random.default_rng(1000 + n)
+    a, b, pi = random_hmm(rng, n)
+    lengths = EDGE_LENGTHS + list(rng.integers(1, 2500, size=40))
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=n, p_n=0.03, p_gap=0.02)
+    t = build_tables(a, b, pi)
+    ll, path, post = run_all(a, b, pi, obs, off)
+    np.testing.assert_allclose(ll, O.forward_loglik(t, obs, off), rtol=RTOL, atol=0)
+    np.testing.assert_array_equal(path, O.viterbi(t, obs, off))
+    np.testing.assert_allclose(post, O.posterior(t, obs, off), rtol=RTOL, atol=1e-300)
+    np.testing.assert_allclose(post.sum(1), 1.0, rtol=1e-12)
+
+
+def test_ties_first_maximum(gpu):
+    """Uniform transitions and duplicated emission rows make many exact ties; the device
+    must resolve every one to the lowest state like np.argmax (optimizer.py:331,346)."""
+    rng = np.random.default_rng(5)
+    n = 70
+    a = np.full((n, n), 1.0 / n)
+    b = rng.dirichlet(np.full(256, 0.5), size=n // 2)
+    b = np.repeat(b, 2, axis=0)
+    pi = np.full(n, 1.0 / n)
+    obs, off, _ = sample_alignment(a, b, pi, [1, 300, 700, 1], seed=9)
+    t = build_tables(a, b, pi)
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    np.testing.assert_array_equal(hmm._paths(model, plan, obs), O.viterbi(t, obs, off))
+
+
+def test_tie_rescan_path_is_exact(gpu, monkeypatch):
+    """The kernel skips the `+ log e_j` add and re-scans a state only when it cannot prove
+    the argmax unchanged; forcing the re-scan for every state must give the same paths."""
+    rng = np.random.default_rng(11)
+    a, b, pi = random_hmm(rng, 70)
+    obs, off, _ = sample_alignment(a, b, pi, [3000, 1, 2000, 600], seed=4)
+    model = hmm.Model(a, b, pi)
+    fast = hmm._paths(model, hmm.Plan(off), obs)
+    monkeypatch.setenv("ITR_FORCE_SLOW_TIES", "1")
+    slow = hmm._paths(model, hmm.Plan(off), obs)
+    monkeypatch.delenv("ITR_FORCE_SLOW_TIES")
+    hmm.Plan(off)  # resets the hook
+    np.testing.assert_array_equal(fast, slow)
+    np.testing.assert_array_equal(fast, O.viterbi(build_tables(a, b, pi), obs, off))
+
+
+@pytest.mark.parametrize("name", [m for m in model_fixtures() if m != "model_kat_1_1.npz"])
+def test_reference_models_vs_oracle(gpu, name):
+    """The reference's own model builds (a, b, pi from trans_emiss_calc) on sampled data."""
+    g = golden(name)
+    a, b, pi = g["a"], g["b"], g["pi"]
+    rng = np.random.default_rng(3)
+    lengths = list(rng.geometric(1 / 1500, size=30)) + [1, 5000]
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=7)
+    t = build_tables(a, b, pi)
+    ll, path, post = run_all(a, b, pi, obs, off)
+    np.testing.assert_allclose(ll, O.forward_loglik(t, obs, off), rtol=RTOL, atol=0)
+    np.testing.assert_array_equal(path, O.viterbi(t, obs, off))
+    np.testing.assert_allclose(post, O.posterior(t, obs, off), rtol=RTOL, atol=1e-300)
+
+
+def test_reference_layer_api(gpu):
+    """optimizer.py-shaped wrappers: types and block-order summation."""
+    g = golden("sweep_syn27.npz")
+    a, b, pi, obs, off = g["a"], g["b"], g["pi"], g["obs"], g["off"]
+    V_lst = [obs[off[k]:off[k + 1]].astype(np.int64) for k in range(len(off) - 1)]
+    acc = 0
+    for v in g["loglik"].tolist():
+        acc += v
+    tot = hmm.loglik_wrapper(a, b, pi, V_lst)
+    assert isinstance(tot, float)
+    assert abs(tot - acc) <= 1e-10 * abs(acc)
+    paths = hmm.viterbi_wrapper(a, b, pi, V_lst)
+    assert all(p.dtype == np.float64 for p in paths)
+    np.testing.assert_array_equal(np.concatenate(paths), g["path"].astype(np.float64))
+    posts = hmm.post_prob_wrapper(a, b, pi, V_lst)
+    assert [p.shape for p in posts] == [(len(v), a.shape[0]) for v in V_lst]
+    assert abs(hmm.forward_loglik(a, b, pi, V_lst[2]) - g["loglik"][2]) <= 1e-10 * abs(acc)
+    with pytest.raises(IndexError):
+        hmm.loglik_wrapper(a, b, pi, [np.array([0, 625])])
+
+
+def test_device_layer_matches_host_layer(gpu):
+    import torch
+
+    g = golden("sweep_syn70.npz")
+    model, plan = hmm.Model(g["a"], g["b"], g["pi"]), hmm.Plan(g["off"])
+    d_obs = torch.from_numpy(g["obs"].astype(np.int16)).to(gpu)
+    ll = hmm.forward_loglik_device(model, plan, d_obs).cpu().numpy()
+    path = hmm.viterbi_device(model, plan, d_obs).cpu().numpy()
+    post = hmm.posterior_device(model, plan, d_obs).cpu().numpy()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(ll, hmm.block_logliks(model, plan, g["obs"]))
+    np.testing.assert_array_equal(path, g["path"])
+    np.testing.assert_array_equal(post, hmm._posteriors(model, plan, g["obs"]))
+    assert hmm.last_kernel_ms("viterbi") > 0

@@ -1,0 +1,31 @@
+"""The CPU oracle (oracle/hmm_oracle.c) pinned against the reference's own outputs.
+
+tests/golden/sweep_*.npz hold forward_loglik / viterbi+backtrack / post_prob results the
+reference produced (tests/golden/make_golden.py).  The oracle is the checker for the device
+sweeps, so it must reproduce them first: loglik to 1e-12 relative, Viterbi paths exactly.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden, sweep_fixtures
+from itrails_amd.tables import build_tables
+from oracle import hmm_oracle as O
+
+
+@pytest.mark.parametrize("name", sweep_fixtures())
+def test_oracle_vs_reference(name):
+    g = golden(name)
+    t = build_tables(g["a"], g["b"], g["pi"])
+    ll = O.forward_loglik(t, g["obs"], g["off"])
+    np.testing.assert_allclose(ll, g["loglik"], rtol=1e-12, atol=0)
+    path = O.viterbi(t, g["obs"], g["off"])
+    np.testing.assert_array_equal(path, g["path"])
+    post = O.posterior(t, g["obs"], g["off"])
+    np.testing.assert_allclose(post[g["post_rows"]], g["post"], rtol=1e-9, atol=1e-300)
+
+
+def test_fixture_paths_switch_states():
+    # a backtracking bug is invisible on paths that never leave one state
+    for name in sweep_fixtures():
+        g = golden(name)
+        assert (np.diff(g["path"]) != 0).sum() > 5, name
