@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--n-int", type=int, default=5)
     ap.add_argument("--mbp", type=float, default=10.0, help="columns per GPU (Mbp)")
     ap.add_argument("--mean-block", type=float, default=2000.0)
-    ap.add_argument("--cpu-sample", type=int, default=400_000,
+    ap.add_argument("--cpu-sample", type=int, default=10_000_000,
                     help="columns of the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--check", action="store_true", help="verify against the CPU oracle")
     args = ap.parse_args()

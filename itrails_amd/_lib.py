@@ -11,7 +11,7 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libitrails_hip.so")
+LIB_PATH = os.environ.get("ITR_LIB") or os.path.join(HERE, "libitrails_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "itrails_hip.h")
 
 ITR_OK, ITR_EINVAL, ITR_EHIP, ITR_ESTATE = 0, 1, 2, 3

@@ -115,6 +115,7 @@ struct itr_plan {
   int64_t *d_off = nullptr, *d_chunk_base = nullptr;
   int32_t *d_order = nullptr, *d_chunk_blk = nullptr;
   int* d_queue = nullptr;
+  int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
   // workspace (grown on demand)
   uint8_t* d_bp = nullptr;
   size_t bp_cap = 0;
@@ -146,14 +147,16 @@ int check_plan(itr_plan_t p) {
 }
 
 int reserve(itr_plan_t p, int n, bool vit, bool post) {
+  const int xr = itr::sweep_row_stride(n);
+  if (xr < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", n);
   if (vit) {
-    const size_t need = (size_t)p->total * n;
+    const size_t need = (size_t)p->total * xr;
     if (need > p->bp_cap) {
       dev_free(p->d_bp);
       if (int e = dev_alloc(&p->d_bp, need)) return e;
       p->bp_cap = need;
     }
-    const size_t needc = (size_t)p->nchunks * n;
+    const size_t needc = (size_t)p->nchunks * xr;
     if (needc > p->cm_cap) {
       dev_free(p->d_chunk_map);
       if (int e = dev_alloc(&p->d_chunk_map, needc)) return e;
@@ -161,7 +164,7 @@ int reserve(itr_plan_t p, int n, bool vit, bool post) {
     }
   }
   if (post) {
-    const size_t need = (size_t)p->total * n;
+    const size_t need = (size_t)p->total * xr;
     if (need > p->alpha_cap) {
       dev_free(p->d_alpha);
       if (int e = dev_alloc(&p->d_alpha, need)) return e;
@@ -180,8 +183,13 @@ itr::SweepArgs base_args(itr_model_t m, itr_plan_t p, const uint16_t* obs) {
   a.queue = p->d_queue;
   a.obs = obs;
   a.chunk_base = p->d_chunk_base;
+  a.prio_len = p->prio_len;
   return a;
 }
+
+#ifdef ITR_DIAG
+uint64_t* g_diag = nullptr;  // diagnostic build: per-segment cycle sums of the last sweep
+#endif
 
 int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname) {
   itr::SweepGeometry g = itr::sweep_geometry(a.n, mode);
@@ -191,6 +199,11 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname) {
   if (grid > a.nblocks) grid = a.nblocks;
   if (grid <= 0) return 0;
   HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
+#ifdef ITR_DIAG
+  if (!g_diag) HIP_TRY(hipMalloc(&g_diag, 16 * sizeof(uint64_t)));
+  HIP_TRY(hipMemsetAsync(g_diag, 0, 16 * sizeof(uint64_t), st));
+  a.diag = g_diag;
+#endif
   {
     Scope sc(tname, st);
     HIP_TRY(itr::launch_sweep(mode, g, (int)grid, a, st));
@@ -198,7 +211,6 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname) {
   return 0;
 }
 
-int g_force_slow = 0;  // test hook (environment ITR_FORCE_SLOW_TIES=1)
 
 }  // namespace
 
@@ -298,6 +310,11 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
     nc += K;
   }
   p->nchunks = nc;
+  if (nblocks > 0) {
+    const int64_t k = std::min<int64_t>(nblocks - 1, 255);
+    const int64_t T = h_off[order[k] + 1] - h_off[order[k]];
+    p->prio_len = (int)std::max<int64_t>(T, 1);
+  }
   int e = 0;
   if (!e) e = dev_alloc(&p->d_off, nblocks + 1);
   if (!e) e = dev_alloc(&p->d_order, nblocks);
@@ -319,8 +336,6 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
     itr_plan_destroy(p);
     return e;
   }
-  const char* fs = getenv("ITR_FORCE_SLOW_TIES");
-  g_force_slow = (fs && fs[0] == '1') ? 1 : 0;
   *out = p;
   return 0;
 }
@@ -383,7 +398,6 @@ int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
   a.bp = p->d_bp;
   a.chunk_map = p->d_chunk_map;
   a.last_state = p->d_last;
-  a.force_slow = g_force_slow;
   if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
   Scope sc("traceback", st);
   HIP_TRY(itr::launch_vit_traceback(m->n, p->nblocks, p->nchunks, p->d_off, p->d_chunk_base,
@@ -475,6 +489,15 @@ int itr_last_kernel_ms(const char* which, double* ms) {
     }
   return fail(ITR_ESTATE, "no timing recorded for '%s'", which);
 }
+
+#ifdef ITR_DIAG
+// diagnostic build only (not part of the ABI): cycle sums of the last sweep
+ITR_API int itr_diag_read(uint64_t* out) {
+  if (!g_diag) return fail(ITR_ESTATE, "no diagnostic data");
+  HIP_TRY(hipMemcpy(out, g_diag, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+#endif
 
 int itr_expm_batched(int n, int64_t batch, const double* A, double* out, void* stream) {
   if (n < 1 || batch < 0) return fail(ITR_EINVAL, "bad expm shape n=%d batch=%lld", n,

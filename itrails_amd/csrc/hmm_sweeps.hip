@@ -4,35 +4,37 @@
 //
 // Work decomposition
 // ------------------
-// A MAF block is a strictly sequential recurrence over its columns, so the only parallelism
-// inside a block is the N x N state contraction of one column step.  One WORKGROUP owns one
-// block at a time (blocks are pulled longest-first from a device work queue, so the long
-// blocks that bound the makespan start first), and splits each step over W = ceil(N/16)
-// wavefronts:
+// A MAF block is a strictly sequential recurrence over its columns: the only parallelism
+// inside a block is the N x N state contraction of one column step, and the longest block
+// bounds the makespan.  One WORKGROUP of exactly four wavefronts — one per SIMD of the CU,
+// so the per-step VALU issue is balanced — owns one block at a time.  Blocks are pulled
+// longest-first from a device work queue, and the longest ones run at raised wave priority
+// (s_setprio) against the co-resident workgroups that work through the short ones.
 //
-//   * wave w produces target states j in [16w, 16w+16): lane l = 8*jl + q holds
-//     j = 16w + 8r + jl for r = 0,1 (RJ = 2 targets per lane, so every LDS broadcast of
-//     x_i feeds two FMAs: the step is VALU-bound, not LDS-bound);
+//   * wave w produces target states j = 8*RJ*w + 8*r + jl (r < RJ slots per lane), lane
+//     l = 8*jl + q;
 //   * the 8 lanes q = 0..7 sharing a j split the source-state sum over i into 8 ranges of
 //     IQ states, i = q*IQ + k.  The lane's IQ x RJ slice of the transition matrix lives in
-//     VGPRs for the whole kernel (no LDS or HBM traffic for `a` in the step loop);
-//   * the 8 partial results are combined with three xor-butterfly shuffles, which gives the
-//     identical (commutative) sum / first-max in all 8 lanes;
-//   * x_{t-1} (the previous column's state vector, N doubles) is the only per-step
-//     exchange: published to LDS, one workgroup barrier, then read back as broadcasts.
+//     VGPRs for the whole kernel (no LDS or HBM traffic for `a` in the step loop); every LDS
+//     broadcast of x_i feeds RJ FMAs;
+//   * the 8 partial results are combined with three DPP stages (quad_perm, quad_perm,
+//     row_half_mirror): no LDS round trip, identical results in all 8 lanes;
+//   * x_{t-1} (N doubles) is the only per-step exchange: published to LDS, one LDS-only
+//     barrier, read back as 16-byte broadcasts.  Cross-wave scalars (rescale maxima, the
+//     posterior row sum) go through one DPP row reduction + 16 LDS partials per step.
+//   * per-column inputs (emission rows, for the posterior also the stored forward rows)
+//     are staged into an LDS ring 16 columns at a time, so the step loop never waits on a
+//     global load; observed symbols are staged 256 at a time.
 //
 // Numerics
 // --------
 // forward / backward run in the probability domain with exact power-of-two rescaling
-// (ldexp of the running maximum's exponent every 8 columns): mathematically identical to
-// the reference's log-space max-shift recursion (optimizer.py:181-187, 205-212), no
+// (ilogb / ldexp of the running maximum every 8 columns): mathematically identical to the
+// reference's log-space max-shift recursion (optimizer.py:181-187, 205-212), no
 // transcendental per state per column, and the rescaling itself is rounding-free.
 // Viterbi is evaluated exactly as optimizer.py:325-330 rounds it — (omega_i + log a_ij)
 // then + log e_j, IEEE adds only, first maximum wins — so paths are bit-identical for
-// identical tables.  The kernel takes the argmax over y_ij = omega_i + log a_ij (one add
-// fewer per pair) and proves, per state, that adding log e_j cannot create an earlier tie
-// (pred(max y) + log e_j < max y + log e_j); if it can, that state is re-scanned with the
-// reference's full expression.
+// identical tables.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -41,30 +43,51 @@
 
 namespace itr {
 
-static constexpr int Q = 8;       // lanes splitting the i-sum of one target state
-static constexpr int J = 64 / Q;  // target states per slot per wave
-static constexpr int RJ = 2;      // slots (target states) per lane
-static constexpr int JW = J * RJ; // target states per wave
-static constexpr int PD = 3;      // emission prefetch depth (columns)
-static constexpr int PDA = 6;     // forward-row prefetch depth in the backward sweep
+static constexpr int W = 4;        // wavefronts per workgroup: one per SIMD
+static constexpr int TB = 64 * W;  // threads per workgroup
+static constexpr int Q = 8;        // lanes splitting the i-sum of one target state
+static constexpr int TE = 16;      // columns per staged tile of per-column rows
 static constexpr double LN2 = 0.69314718055994530942;
+
+// Diagnostic build only (-DITR_DIAG, libitrails_hip_diag.so): wave 0 of every workgroup
+// accumulates shader-clock cycles per step segment; never compiled into the product.
+#ifdef ITR_DIAG
+#define DIAG_DECL uint64_t dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t dlast = 0; uint64_t dsteps = 0;
+#define STAMP(i)                                                   \
+  do {                                                             \
+    __builtin_amdgcn_sched_barrier(0);                             \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();            \
+    __builtin_amdgcn_sched_barrier(0);                             \
+    if ((i) >= 0) dsum[(i) < 0 ? 0 : (i)] += now_ - dlast;         \
+    dlast = now_;                                                  \
+  } while (0)
+#define DIAG_STEP() (++dsteps)
+#define DIAG_FLUSH()                                                          \
+  do {                                                                        \
+    if (tid == 0 && p.diag) {                                                 \
+      for (int i_ = 0; i_ < 8; ++i_) atomicAdd((unsigned long long*)&p.diag[i_], \
+                                               (unsigned long long)dsum[i_]);  \
+      atomicAdd((unsigned long long*)&p.diag[8], (unsigned long long)dsteps);   \
+    }                                                                         \
+  } while (0)
+#else
+#define DIAG_DECL
+#define STAMP(i)
+#define DIAG_STEP()
+#define DIAG_FLUSH()
+#endif
 
 // ---------------------------------------------------------------------------------------
 // small device helpers
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v = fmax(v, __shfl_xor(v, d));
-  return v;
-}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
   return v;
 }
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-
-// first-maximum reduction key over the wave: larger value wins, equal values -> lower index
+// first-maximum reduction over the wave: larger value wins, equal values -> lower index
 __device__ __forceinline__ void wave_first_max(double& v, int& idx) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
@@ -76,487 +99,604 @@ __device__ __forceinline__ void wave_first_max(double& v, int& idx) {
   }
 }
 
-// Tile of observed symbols staged in LDS.  Tiles hold TB = blockDim.x consecutive STEPS of
-// the sweep (forward: columns s; backward: columns T-1-s); two tiles are resident and the
-// one after them is in flight in a register of every thread, so a global load is waited
-// for one whole tile (TB steps) after it was issued.
+// DPP cross-lane moves (a VALU operand modifier: a few cycles, no LDS round trip).
+// Within the 8 lanes q = l & 7 of one target state: stage 1 pairs q with q^1, stage 2 with
+// q^2 (quad_perm), stage 3 with 7-q (row_half_mirror).  Across the two target states of a
+// 16-lane row: row_ror:8.
+static constexpr int DPP_Q1 = 0xB1;   // quad_perm [1,0,3,2]
+static constexpr int DPP_Q2 = 0x4E;   // quad_perm [2,3,0,1]
+static constexpr int DPP_HM = 0x141;  // row_half_mirror
+static constexpr int DPP_R8 = 0x128;  // row_ror:8
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = dpp_i32<CTRL>(__double2loint(v));
+  const int hi = dpp_i32<CTRL>(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+// after the three stages all 8 lanes hold ((a0+a1)+(a2+a3))+((a4+a5)+(a6+a7)): every
+// addition is commutative, so the 8 copies are bit-identical
+template <int RJN>
+__device__ __forceinline__ void combine_sum(double (&acc)[RJN]) {
+#pragma unroll
+  for (int r = 0; r < RJN; ++r) acc[r] += dpp_f64<DPP_Q1>(acc[r]);
+#pragma unroll
+  for (int r = 0; r < RJN; ++r) acc[r] += dpp_f64<DPP_Q2>(acc[r]);
+#pragma unroll
+  for (int r = 0; r < RJN; ++r) acc[r] += dpp_f64<DPP_HM>(acc[r]);
+}
+// First maximum over the 8 lanes of a target state.  The maximum value is reduced first
+// (fmax is exact and order-free), then the winning index is the smallest arg among the
+// lanes whose own maximum equals it: lanes hold increasing i ranges and each lane's arg is
+// already its first maximum, so the minimum such arg is the first maximum overall.
+// All 8 lanes end with identical (best, arg).
+template <int RJN>
+__device__ __forceinline__ void combine_first_max(double (&best)[RJN], int (&arg)[RJN]) {
+  double mx[RJN];
+#pragma unroll
+  for (int r = 0; r < RJN; ++r) mx[r] = fmax(best[r], dpp_f64<DPP_Q1>(best[r]));
+#pragma unroll
+  for (int r = 0; r < RJN; ++r) mx[r] = fmax(mx[r], dpp_f64<DPP_Q2>(mx[r]));
+#pragma unroll
+  for (int r = 0; r < RJN; ++r) mx[r] = fmax(mx[r], dpp_f64<DPP_HM>(mx[r]));
+  int a[RJN];
+#pragma unroll
+  for (int r = 0; r < RJN; ++r) a[r] = (best[r] == mx[r]) ? arg[r] : 0x7fffffff;
+#pragma unroll
+  for (int r = 0; r < RJN; ++r) a[r] = min(a[r], dpp_i32<DPP_Q1>(a[r]));
+#pragma unroll
+  for (int r = 0; r < RJN; ++r) a[r] = min(a[r], dpp_i32<DPP_Q2>(a[r]));
+#pragma unroll
+  for (int r = 0; r < RJN; ++r) a[r] = min(a[r], dpp_i32<DPP_HM>(a[r]));
+#pragma unroll
+  for (int r = 0; r < RJN; ++r) {
+    best[r] = mx[r];
+    arg[r] = a[r];
+  }
+}
+
+// s_waitcnt vmcnt(0) (expcnt/lgkmcnt untouched).  Issued once before each step loop so
+// that no loop-carried register is the destination of a load in flight at loop entry:
+// otherwise hipcc's waitcnt pass puts a vmcnt(0) INSIDE the loop at that register's first
+// use, which then drains the staged-row and symbol loads every column.
+__device__ __forceinline__ void wait_vmem_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup-scope fence
+// over ALL address spaces, which on gfx950 drains vmcnt to 0 at every column: it would wait
+// for the back-pointer / forward-row stores and the staged-row loads each step.  All
+// inter-wave exchange in this kernel goes through LDS, so the fences are "local" only.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Observed symbols of the current block staged in LDS, 256 steps per tile (forward: step s
+// is column s; backward: column T-1-s).  Two tiles are resident and the next one is in
+// flight in a register of every thread, so its global load is waited for 256 steps after
+// it was issued.
 struct ObsTiles {
-  uint16_t* lds;     // [2][TB]
-  const uint16_t* g; // block's first column
-  int T, TB, dir;    // dir = +1 forward, -1 backward
-  int inflight;      // this thread's element of the next tile to store
+  uint16_t* lds;      // [2][TB]
+  const uint16_t* g;  // block's first column
+  int T, dir;         // dir = +1 forward, -1 backward
+  int inflight;       // this thread's element of the next tile to store
 
   __device__ __forceinline__ int col(int s) const { return dir > 0 ? s : T - 1 - s; }
-  // symbols outside the 625-letter alphabet are clamped (memory safety; the host
-  // wrappers reject them before they reach the device)
   __device__ __forceinline__ int fetch(int s) const {
-    return (s >= 0 && s < T) ? min((int)g[col(s)], 624) : 0;
+    return (s >= 0 && s < T) ? (int)g[col(s)] : 0;
   }
-  // block start: tiles 0 and 1 into LDS, tile 2 in flight
-  __device__ __forceinline__ void start(int tid) {
-    lds[tid] = (uint16_t)fetch(tid);
-    lds[TB + tid] = (uint16_t)fetch(TB + tid);
+  // symbols outside the 625-letter alphabet are clamped (memory safety; the host wrappers
+  // reject them before they reach the device)
+  __device__ __forceinline__ static uint16_t clamp(int v) { return (uint16_t)min(v, 624); }
+  __device__ __forceinline__ void start(int tid) {  // tiles 0, 1 in LDS; tile 2 in flight
+    lds[tid] = clamp(fetch(tid));
+    lds[TB + tid] = clamp(fetch(TB + tid));
     inflight = fetch(2 * TB + tid);
   }
-  // call at step s (before the step's barrier); when s starts tile k >= 1, tile k+1 is
-  // stored into the slot tile k-1 used, and tile k+2 is requested
+  // at step s (before the step's barrier): when s starts tile k >= 1, tile k+1 replaces
+  // tile k-1 and tile k+2 is requested
   __device__ __forceinline__ void advance(int s, int tid) {
-    if (s >= TB && (s % TB) == 0) {
+    if (s >= TB && (s & (TB - 1)) == 0) {
       const int k = s / TB;
-      lds[((k + 1) & 1) * TB + tid] = (uint16_t)inflight;
+      lds[((k + 1) & 1) * TB + tid] = clamp(inflight);
       inflight = fetch((k + 2) * TB + tid);
     }
   }
   __device__ __forceinline__ int get(int s) const {  // symbol at step s (LDS broadcast)
-    return (s < T) ? (int)lds[((s / TB) & 1) * TB + (s % TB)] : 0;
+    return (s < T) ? (int)lds[((s / TB) & 1) * TB + (s & (TB - 1))] : 0;
+  }
+};
+
+// Rows of a global row-major table (E / log E by observed symbol, or stored forward rows by
+// column) for TE consecutive steps, loaded into registers one tile ahead and committed to an
+// LDS ring [2][TE][XR] at the tile boundary.  Element idx = tid + e*TB of a tile is row
+// idx / XR, target state idx % XR.
+template <int RJN>
+struct RowStage {
+  static constexpr int XR = 32 * RJN;      // padded target states
+  static constexpr int RS = TE * XR / TB;  // = 2 * RJN elements per thread
+  double v[RS];
+  template <class RowOf>
+  __device__ __forceinline__ void issue(const double* __restrict__ g, int stride, int ncol,
+                                        int tid, int s0, RowOf row_of) {
+#pragma unroll
+    for (int e = 0; e < RS; ++e) {
+      const int idx = tid + e * TB;
+      const int row = idx / XR, col = idx % XR;
+      const int64_t src = row_of(s0 + row);
+      v[e] = (src >= 0 && col < ncol) ? g[src * stride + col] : 0.0;
+    }
+  }
+  __device__ __forceinline__ void commit(double* lds_tile, int tid) const {
+#pragma unroll
+    for (int e = 0; e < RS; ++e) lds_tile[e * TB + tid] = v[e];
   }
 };
 
 // ---------------------------------------------------------------------------------------
-// the sweep kernel
+// the sweep kernel: RJN target states per lane, IQ source states per lane
 // ---------------------------------------------------------------------------------------
-// threads of the widest workgroup an IQ serves: N <= 8*IQ states -> ceil(N/16) waves
-template <int IQ>
-struct MaxBlock {
-  static constexpr int value = 64 * ((Q * IQ + JW - 1) / JW);
+// co-resident workgroups per CU the register budget is sized for (one wave per SIMD each)
+template <int RJN, int IQ, int MODE>
+struct Occ {
+  static constexpr int base = RJN * IQ <= 27 ? 3 : RJN * IQ <= 64 ? 2 : 1;
+  static constexpr int value = (MODE == MODE_BWD && base > 1) ? base - 1 : base;
 };
 
-template <int IQ, int MODE>
-__global__ void __launch_bounds__(MaxBlock<IQ>::value) sweep_kernel(SweepArgs p) {
+template <int RJN, int IQ, int MODE>
+__global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(SweepArgs p) {
+  constexpr int IQS = IQ + (IQ & 1);  // 16-byte aligned source ranges in LDS
+  constexpr int XS = Q * IQS;         // published vector length
+  constexpr int JW = 8 * RJN;         // target states per wave
+  constexpr int XR = W * JW;          // padded target states per workgroup
+  constexpr int NCH = IQ >= 6 ? 3 : (IQ >= 2 ? 2 : 1);  // independent chains per target
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = p.n;
-  const int XP = p.xp;  // padded state count of the LDS vectors (multiple of 16)
   const int tid = threadIdx.x;
-  const int TB = blockDim.x;
-  const int W = TB >> 6;
   const int w = uni(tid >> 6);
   const int l = tid & 63;
   const int q = l & (Q - 1);
   const int jl = l >> 3;
+  const int row16 = w * 4 + (l >> 4);  // 16-lane row of the workgroup (0..15)
+  const bool row_leader = (l & 15) == 0;
 
-  double* X = reinterpret_cast<double*>(smem);  // [2][XP]  published state vectors
-  double* RED = X + 2 * XP;                     // [4][16]  per-wave partials (2 kinds x 2 bufs)
-  int* SBLK = reinterpret_cast<int*>(RED + 64); // [4]      current block
-  int* REDI = SBLK + 4;                         // [16]     per-wave argmax
-  uint16_t* OBS = reinterpret_cast<uint16_t*>(REDI + 16);           // [2][TB]
-  uint8_t* ORIG = reinterpret_cast<uint8_t*>(OBS + 2 * TB);          // [2][XP] (Viterbi)
+  double* X = reinterpret_cast<double*>(smem);  // [2][XS+64]    published vectors + a
+                                                //               per-lane write sink
+  double* RED = X + 2 * (XS + 64);              // [4][16]       row partials
+  double* EST = RED + 64;                       // [2][TE][XR]   staged emission rows
+  double* AST = EST + 2 * TE * XR;              // [2][TE][XR]   staged forward rows (BWD)
+  int* SBLK = reinterpret_cast<int*>(AST + ((MODE == MODE_BWD) ? 2 * TE * XR : 0));
+  int* REDI = SBLK + 4;                                      // [4]
+  uint16_t* OBS = reinterpret_cast<uint16_t*>(SBLK + 32);    // [2][TB]
+  uint8_t* ORIG = reinterpret_cast<uint8_t*>(OBS + 2 * TB);  // [2][256+64] (Viterbi)
 
-  int jr[RJ];
-  bool jv[RJ];
+  // Publishing is branch-free: the one lane (q == 0) of a real target state writes its
+  // slot, every other lane writes the same value into its own sink entry nobody reads.
+  int jr[RJN], jx[RJN], jo[RJN];
+  bool jv[RJN];
 #pragma unroll
-  for (int r = 0; r < RJ; ++r) {
-    jr[r] = w * JW + r * J + jl;
+  for (int r = 0; r < RJN; ++r) {
+    jr[r] = w * JW + r * 8 + jl;
     jv[r] = jr[r] < n;
+    const bool pub = jv[r] && q == 0;
+    jx[r] = pub ? (jr[r] / IQ) * IQS + jr[r] % IQ : XS + l;  // slot of state jr in X
+    jo[r] = pub ? jr[r] : 256 + l;                            // slot of state jr in ORIG
   }
 
   // this lane's slice of a (or log a): rows i = q*IQ + k, columns jr[r]
-  double m[IQ][RJ];
+  double m[IQ][RJN];
 #pragma unroll
   for (int k = 0; k < IQ; ++k) {
     const int i = q * IQ + k;
 #pragma unroll
-    for (int r = 0; r < RJ; ++r)
+    for (int r = 0; r < RJN; ++r)
       m[k][r] = (i < n && jv[r]) ? p.mat[(int64_t)i * n + jr[r]] : 0.0;
   }
 
-  // padding of the published vectors (entries no lane ever writes): 0 for the
-  // probability sweeps (contributes nothing), -inf for Viterbi (never a maximum)
+  // published entries of states >= n are never written: 0 for the probability sweeps
+  // (contributes nothing), -inf for Viterbi (never a maximum)
   const double pad = (MODE == MODE_VIT) ? -INFINITY : 0.0;
-  for (int i = tid; i < 2 * XP; i += TB) X[i] = pad;
-  __syncthreads();
+  for (int i = tid; i < 2 * (XS + 64); i += TB) X[i] = pad;
+  lds_barrier();
+
+  RowStage<RJN> est;
+  RowStage<RJN> ast;
+  (void)ast;
+  DIAG_DECL
 
   for (;;) {
     if (tid == 0) SBLK[0] = atomicAdd(p.queue, 1);
-    __syncthreads();
+    lds_barrier();
     const int bi = uni(SBLK[0]);
-    __syncthreads();
+    lds_barrier();
     if (bi >= p.nblocks) break;
     const int blk = uni(p.order[bi]);
     const int64_t c0 = p.off[blk];
     const int T = uni((int)(p.off[blk + 1] - c0));
+    // NOTE: no `continue` in this loop.  With a barrier in the body, hipcc (ROCm 7.2)
+    // structurizes a `continue` back to the head's `if (tid == 0)` as a lane-divergent
+    // inner loop around the barrier, which deadlocks the workgroup.
     if (T <= 0) {  // empty block: log-likelihood of nothing is 0, no other output
       if (MODE == MODE_FWD_LL && tid == 0) p.loglik[blk] = 0.0;
-      continue;
-    }
-
-    ObsTiles ot{OBS, p.obs + c0, T, TB, (MODE == MODE_BWD) ? -1 : +1, 0};
-    ot.start(tid);
-    __syncthreads();
-
-    if constexpr (MODE == MODE_FWD_LL || MODE == MODE_FWD_STORE) {
-      // ---------------- forward: alpha_t = (alpha_{t-1} @ a) * e_t  (optimizer.py:181-187)
-      const int o0 = ot.get(0);
-      double x[RJ];
-#pragma unroll
-      for (int r = 0; r < RJ; ++r) x[r] = jv[r] ? p.init[o0 * n + jr[r]] : 0.0;
-      if (MODE == MODE_FWD_STORE && q == 0) {
-#pragma unroll
-        for (int r = 0; r < RJ; ++r)
-          if (jv[r]) p.alpha[c0 * n + jr[r]] = x[r];
+    } else {
+      const bool urgent = T >= p.prio_len;
+      if (urgent) __builtin_amdgcn_s_setprio(2);
+      ObsTiles ot{OBS, p.obs + c0, T, (MODE == MODE_BWD) ? -1 : +1, 0};
+      ot.start(tid);
+      lds_barrier();
+      auto sym_row = [&](int s) -> int64_t { return s < T ? (int64_t)ot.get(s) : -1; };
+      auto fwd_row = [&](int s) -> int64_t { return s < T ? c0 + (T - 1 - s) : -1; };
+      est.issue(p.emit, n, n, tid, 0, sym_row);
+      est.commit(EST, tid);
+      est.issue(p.emit, n, n, tid, TE, sym_row);
+      if constexpr (MODE == MODE_BWD) {
+        ast.issue(p.alpha, XR, XR, tid, 0, fwd_row);
+        ast.commit(AST, tid);
+        ast.issue(p.alpha, XR, XR, tid, TE, fwd_row);
       }
-      double ering[PD][RJ];
-#pragma unroll
-      for (int d = 0; d < PD; ++d) {
-        const int o = ot.get(1 + d);
-#pragma unroll
-        for (int r = 0; r < RJ; ++r)
-          ering[d][r] = (1 + d < T && jv[r]) ? p.emit[o * n + jr[r]] : 0.0;
-      }
-      int K = 0;  // sum of the power-of-two exponents divided out so far
-      int buf = 0;
-      for (int t = 1; t < T; ++t) {
-        double* Xb = X + buf * XP;
-        if (q == 0) {
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) Xb[jr[r]] = x[r];
+      // a new staged tile starts at step s: commit it before the step's barrier ...
+      auto stage_commit = [&](int s) {
+        if (s >= TE && (s & (TE - 1)) == 0) {
+          const int slot = (s / TE) & 1;
+          est.commit(EST + slot * TE * XR, tid);
+          if constexpr (MODE == MODE_BWD) ast.commit(AST + slot * TE * XR, tid);
         }
-        const bool rescale = (t & 7) == 1;
-        if (rescale) {
-          double mx = x[0];
-#pragma unroll
-          for (int r = 1; r < RJ; ++r) mx = fmax(mx, x[r]);
-          mx = wave_max(mx);
-          if (l == 0) RED[buf * 16 + w] = mx;
+      };
+      // ... and request the one after it behind the barrier
+      auto stage_issue = [&](int s) {
+        if (s >= TE && (s & (TE - 1)) == 0) {
+          est.issue(p.emit, n, n, tid, s + TE, sym_row);
+          if constexpr (MODE == MODE_BWD) ast.issue(p.alpha, XR, XR, tid, s + TE, fwd_row);
         }
-        ot.advance(t, tid);
-        __syncthreads();
-        double s = 1.0;
-        if (rescale) {
-          double M = RED[buf * 16];
-          for (int v = 1; v < W; ++v) M = fmax(M, RED[buf * 16 + v]);
-          if (M > 0.0 && M < INFINITY) {
-            const int e = ilogb(M);
-            s = ldexp(1.0, -e);
-            K += e;
+      };
+      auto staged = [&](const double* base, int s, int j) {
+        return base[((s / TE) & 1) * TE * XR + (s & (TE - 1)) * XR + j];
+      };
+      lds_barrier();
+
+      if constexpr (MODE == MODE_FWD_LL || MODE == MODE_FWD_STORE) {
+        // ------------- forward: alpha_t = (alpha_{t-1} @ a) * e_t  (optimizer.py:181-187)
+        // Rows written to p.alpha (posterior workspace) have stride XR: every lane stores,
+        // padded states store 0, duplicates store the same value (no branches).
+        const int o0 = ot.get(0);
+        double x[RJN];
+#pragma unroll
+        for (int r = 0; r < RJN; ++r) x[r] = jv[r] ? p.init[o0 * n + jr[r]] : 0.0;
+        if constexpr (MODE == MODE_FWD_STORE) {
+#pragma unroll
+          for (int r = 0; r < RJN; ++r) p.alpha[c0 * XR + jr[r]] = x[r];
+        }
+        int K = 0;  // sum of the power-of-two exponents divided out so far
+        wait_vmem_all();
+        STAMP(-1);
+        // steps in tiles of TE: the periodic work sits at compile-time positions of the
+        // unrolled tile, so a normal step executes no taken branch
+        for (int t0 = 0; t0 < T; t0 += TE) {
+#pragma unroll
+          for (int sub = 0; sub < TE; ++sub) {
+            const int t = t0 + sub;
+            if (t >= 1 && t < T) {
+              DIAG_STEP();
+              const int buf = sub & 1;  // t0 is even
+              double* Xb = X + buf * (XS + 64);
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) Xb[jx[r]] = x[r];
+              const bool rescale = (sub & 7) == 1;
+              if (rescale) {  // row maxima of x_{t-1} (padded states hold 0)
+                double mx = x[0];
+#pragma unroll
+                for (int r = 1; r < RJN; ++r) mx = fmax(mx, x[r]);
+                mx = fmax(mx, dpp_f64<DPP_R8>(mx));
+                if (row_leader) RED[buf * 16 + row16] = mx;
+              }
+              // emission factors of column t: staged at the start of this tile, so (except
+              // on the tile's first step, which commits them) readable before the barrier
+              double ec[RJN];
+              if (sub != 0) {
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) ec[r] = staged(EST, t, jr[r]);
+              }
+              if (sub == 0) {
+                ot.advance(t, tid);
+                stage_commit(t);
+              }
+              STAMP(0);
+              lds_barrier();
+              STAMP(1);
+              if (sub == 0) {
+                stage_issue(t);
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) ec[r] = staged(EST, t, jr[r]);
+              }
+              const double* xs = Xb + q * IQS;
+              // NCH independent partial sums per target (k = c mod NCH): the dependent
+              // FP64 chain is ceil(IQ/NCH) long instead of IQ
+              double acc[NCH][RJN];
+#pragma unroll
+              for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) acc[c][r] = 0.0;
+#pragma unroll
+              for (int k = 0; k < IQ; ++k) {
+                const double xi = xs[k];
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) acc[k % NCH][r] = fma(xi, m[k][r], acc[k % NCH][r]);
+              }
+              if (rescale) {  // fold 2^-e into the emission factor (off the FMA chain)
+                double M = RED[buf * 16];
+#pragma unroll
+                for (int v = 1; v < 16; ++v) M = fmax(M, RED[buf * 16 + v]);
+                const bool ok = M > 0.0 && M < INFINITY;
+                const int e = ok ? ilogb(M) : 0;
+                const double sc = ldexp(1.0, -e);
+                K += e;
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) ec[r] *= sc;
+              }
+              double sum[RJN];
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) {
+                sum[r] = acc[0][r];
+#pragma unroll
+                for (int c = 1; c < NCH; ++c) sum[r] += acc[c][r];
+              }
+              STAMP(2);
+              combine_sum(sum);
+              STAMP(3);
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) x[r] = sum[r] * ec[r];
+              STAMP(4);
+              if constexpr (MODE == MODE_FWD_STORE) {
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) p.alpha[(c0 + t) * XR + jr[r]] = x[r];
+              }
+              STAMP(5);
+            }
           }
         }
-        double ec[RJ];
-#pragma unroll
-        for (int r = 0; r < RJ; ++r) ec[r] = ering[0][r];
-#pragma unroll
-        for (int d = 0; d + 1 < PD; ++d)
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) ering[d][r] = ering[d + 1][r];
-        {
-          const int tn = t + PD;
-          const int o = ot.get(tn);
-#pragma unroll
-          for (int r = 0; r < RJ; ++r)
-            ering[PD - 1][r] = (tn < T && jv[r]) ? p.emit[o * n + jr[r]] : 0.0;
-        }
-        double acc[RJ];
-#pragma unroll
-        for (int r = 0; r < RJ; ++r) acc[r] = 0.0;
-        const double* xs = Xb + q * IQ;
-#pragma unroll
-        for (int k = 0; k < IQ; ++k) {
-          const double xi = xs[k];
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) acc[r] = fma(xi, m[k][r], acc[r]);
-        }
-#pragma unroll
-        for (int d = 1; d < Q; d <<= 1)
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) acc[r] += __shfl_xor(acc[r], d);
-#pragma unroll
-        for (int r = 0; r < RJ; ++r) x[r] = (acc[r] * ec[r]) * s;
-        if (MODE == MODE_FWD_STORE && q == 0) {
-#pragma unroll
-          for (int r = 0; r < RJ; ++r)
-            if (jv[r]) p.alpha[(c0 + t) * n + jr[r]] = x[r];
-        }
-        buf ^= 1;
-      }
-      if constexpr (MODE == MODE_FWD_LL) {
-        // log P = log(sum_j x_j) + K ln 2   (optimizer.py:160-162)
-        double part = 0.0;
-        if (q == 0) {
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) part += jv[r] ? x[r] : 0.0;
-        }
-        part = wave_sum(part);
-        if (l == 0) RED[buf * 16 + w] = part;
-        __syncthreads();
-        if (tid == 0) {
-          double tot = 0.0;
-          for (int v = 0; v < W; ++v) tot += RED[buf * 16 + v];
-          p.loglik[blk] = log(tot) + (double)K * LN2;
-        }
-      }
-    } else if constexpr (MODE == MODE_BWD) {
-      // ---------------- backward + posterior (optimizer.py:191-238)
-      //   beta_{T-1} = 1;  beta_{t-1} = (beta_t * e_t) @ a   (vector @ a: the reference's form)
-      //   post_t = alpha_t * beta_t / sum_j(alpha_t * beta_t)
-      double bt[RJ];
-#pragma unroll
-      for (int r = 0; r < RJ; ++r) bt[r] = jv[r] ? 1.0 : 0.0;
-      // step s handles column t = T-1-s
-      double ering[PD][RJ];
-      double aring[PDA][RJ];
-#pragma unroll
-      for (int d = 0; d < PD; ++d) {
-        const int o = ot.get(d);
-#pragma unroll
-        for (int r = 0; r < RJ; ++r) ering[d][r] = (d < T && jv[r]) ? p.emit[o * n + jr[r]] : 0.0;
-      }
-#pragma unroll
-      for (int d = 0; d < PDA; ++d) {
-        const int tcol = T - 1 - d;
-#pragma unroll
-        for (int r = 0; r < RJ; ++r)
-          aring[d][r] = (tcol >= 0 && jv[r]) ? p.alpha[(c0 + tcol) * n + jr[r]] : 0.0;
-      }
-      int buf = 0;
-      for (int s = 0; s < T; ++s) {
-        const int t = T - 1 - s;
-        double qv[RJ], part = 0.0;
-#pragma unroll
-        for (int r = 0; r < RJ; ++r) {
-          qv[r] = aring[0][r] * bt[r];
-          part += (q == 0) ? qv[r] : 0.0;
-        }
-        part = wave_sum(part);
-        if (l == 0) RED[buf * 16 + w] = part;
-        double* Xb = X + buf * XP;
-        const bool more = t > 0;
-        const bool rescale = (s & 7) == 0;
-        double ec[RJ];
-#pragma unroll
-        for (int r = 0; r < RJ; ++r) ec[r] = ering[0][r];
-        if (more) {
-          double v[RJ];
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) v[r] = bt[r] * ec[r];
+        if constexpr (MODE == MODE_FWD_LL) {
+          // log P = log(sum_j x_j) + K ln 2   (optimizer.py:160-162)
+          double part = 0.0;
           if (q == 0) {
 #pragma unroll
-            for (int r = 0; r < RJ; ++r) Xb[jr[r]] = v[r];
+            for (int r = 0; r < RJN; ++r) part += jv[r] ? x[r] : 0.0;
           }
-          if (rescale) {
-            double mx = fmax(v[0], v[1]);
-            mx = wave_max(mx);
-            if (l == 0) RED[32 + buf * 16 + w] = mx;
-          }
-        }
-        if (s > 0) ot.advance(s, tid);
-        __syncthreads();
-        double S = 0.0;
-        for (int u = 0; u < W; ++u) S += RED[buf * 16 + u];
-        if (q == 0) {
+          part = wave_sum(part);
+          if (l == 0) RED[32 + w] = part;
+          lds_barrier();
+          if (tid == 0) {
+            double tot = 0.0;
 #pragma unroll
-          for (int r = 0; r < RJ; ++r)
-            if (jv[r]) p.post[(c0 + t) * n + jr[r]] = qv[r] / S;
-        }
-        if (more) {
-          double sc = 1.0;
-          if (rescale) {
-            double M = RED[32 + buf * 16];
-            for (int u = 1; u < W; ++u) M = fmax(M, RED[32 + buf * 16 + u]);
-            if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
-          }
-          // rotate prefetch rings
-#pragma unroll
-          for (int d = 0; d + 1 < PD; ++d)
-#pragma unroll
-            for (int r = 0; r < RJ; ++r) ering[d][r] = ering[d + 1][r];
-          {
-            const int sn = s + PD;
-            const int o = ot.get(sn);
-#pragma unroll
-            for (int r = 0; r < RJ; ++r)
-              ering[PD - 1][r] = (sn < T && jv[r]) ? p.emit[o * n + jr[r]] : 0.0;
-          }
-#pragma unroll
-          for (int d = 0; d + 1 < PDA; ++d)
-#pragma unroll
-            for (int r = 0; r < RJ; ++r) aring[d][r] = aring[d + 1][r];
-          {
-            const int tcol = t - PDA;
-#pragma unroll
-            for (int r = 0; r < RJ; ++r)
-              aring[PDA - 1][r] = (tcol >= 0 && jv[r]) ? p.alpha[(c0 + tcol) * n + jr[r]] : 0.0;
-          }
-          double acc[RJ];
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) acc[r] = 0.0;
-          const double* xs = Xb + q * IQ;
-#pragma unroll
-          for (int k = 0; k < IQ; ++k) {
-            const double xi = xs[k];
-#pragma unroll
-            for (int r = 0; r < RJ; ++r) acc[r] = fma(xi, m[k][r], acc[r]);
-          }
-#pragma unroll
-          for (int d = 1; d < Q; d <<= 1)
-#pragma unroll
-            for (int r = 0; r < RJ; ++r) acc[r] += __shfl_xor(acc[r], d);
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) bt[r] = acc[r] * sc;
-        }
-        buf ^= 1;
-      }
-    } else {
-      // ---------------- Viterbi (optimizer.py:305-333), back-pointers as uint8
-      const int o0 = ot.get(0);
-      double x[RJ];
-#pragma unroll
-      for (int r = 0; r < RJ; ++r) x[r] = jv[r] ? p.init[o0 * n + jr[r]] : -INFINITY;
-      int org[RJ] = {0, 0};
-      double ering[PD][RJ];
-#pragma unroll
-      for (int d = 0; d < PD; ++d) {
-        const int o = ot.get(1 + d);
-#pragma unroll
-        for (int r = 0; r < RJ; ++r)
-          ering[d][r] = (1 + d < T && jv[r]) ? p.emit[o * n + jr[r]] : 0.0;
-      }
-      const int64_t cbase = p.chunk_base[blk];
-      int buf = 0;
-      for (int t = 1; t < T; ++t) {
-        double* Xb = X + buf * XP;
-        uint8_t* Ob = ORIG + buf * XP;
-        if (q == 0) {
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) {
-            Xb[jr[r]] = x[r];
-            Ob[jr[r]] = (uint8_t)org[r];
+            for (int v = 0; v < W; ++v) tot += RED[32 + v];
+            p.loglik[blk] = log(tot) + (double)K * LN2;
           }
         }
-        ot.advance(t, tid);
-        __syncthreads();
-        double ec[RJ];
+      } else if constexpr (MODE == MODE_BWD) {
+        // ------------- backward + posterior (optimizer.py:191-238)
+        //   beta_{T-1} = 1;  beta_{t-1} = (beta_t * e_t) @ a  (vector @ a: the reference's form)
+        //   post_t = alpha_t * beta_t / sum_j(alpha_t * beta_t)
+        double bt[RJN];
 #pragma unroll
-        for (int r = 0; r < RJ; ++r) ec[r] = ering[0][r];
-#pragma unroll
-        for (int d = 0; d + 1 < PD; ++d)
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) ering[d][r] = ering[d + 1][r];
-        {
-          const int tn = t + PD;
-          const int o = ot.get(tn);
-#pragma unroll
-          for (int r = 0; r < RJ; ++r)
-            ering[PD - 1][r] = (tn < T && jv[r]) ? p.emit[o * n + jr[r]] : 0.0;
-        }
-        const double* xs = Xb + q * IQ;
-        double best[RJ];
-        int arg[RJ];
-        {
-          const double x0 = xs[0];
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) {
-            best[r] = x0 + m[0][r];
-            arg[r] = 0;
+        for (int r = 0; r < RJN; ++r) bt[r] = jv[r] ? 1.0 : 0.0;
+        int buf = 0;
+        wait_vmem_all();
+        for (int s = 0; s < T; ++s) {  // step s handles column t = T-1-s
+          const int t = T - 1 - s;
+          if (s >= TE && (s & (TE - 1)) == 0) {  // a new staged tile (and maybe obs tile)
+            ot.advance(s, tid);
+            stage_commit(s);
+            lds_barrier();
+            stage_issue(s);
           }
-        }
+          double qv[RJN], ps = 0.0;
 #pragma unroll
-        for (int k = 1; k < IQ; ++k) {
-          const double xi = xs[k];
-#pragma unroll
-          for (int r = 0; r < RJ; ++r) {
-            const double y = xi + m[k][r];
-            const bool gt = y > best[r];
-            best[r] = gt ? y : best[r];
-            arg[r] = gt ? k : arg[r];
+          for (int r = 0; r < RJN; ++r) {
+            qv[r] = staged(AST, s, jr[r]) * bt[r];  // padded states: 0 * 0
+            ps += qv[r];
           }
-        }
+          ps += dpp_f64<DPP_R8>(ps);  // the row's two target-state groups
+          if (row_leader) RED[buf * 16 + row16] = ps;
+          double* Xb = X + buf * (XS + 64);
+          const bool more = t > 0;
+          const bool rescale = (s & 7) == 0;
+          if (more) {
+            double v[RJN];
 #pragma unroll
-        for (int r = 0; r < RJ; ++r) arg[r] += q * IQ;
-        // combine the 8 i-ranges; on equal maxima the lower range (lower i) wins
+            for (int r = 0; r < RJN; ++r) v[r] = bt[r] * staged(EST, s, jr[r]);
 #pragma unroll
-        for (int d = 1; d < Q; d <<= 1) {
-          const bool partner_hi = (q & d) == 0;
+            for (int r = 0; r < RJN; ++r) Xb[jx[r]] = v[r];
+            if (rescale) {
+              double mx = v[0];
 #pragma unroll
-          for (int r = 0; r < RJ; ++r) {
-            const double ob = __shfl_xor(best[r], d);
-            const int oa = __shfl_xor(arg[r], d);
-            const bool take = partner_hi ? (ob > best[r]) : !(best[r] > ob);
-            best[r] = take ? ob : best[r];
-            arg[r] = take ? oa : arg[r];
+              for (int r = 1; r < RJN; ++r) mx = fmax(mx, v[r]);
+              mx = fmax(mx, dpp_f64<DPP_R8>(mx));
+              if (row_leader) RED[32 + buf * 16 + row16] = mx;
+            }
           }
-        }
-        double Mv[RJ];
-        bool need[RJ];
-        bool any_need = false;
+          lds_barrier();
+          double S = 0.0;
 #pragma unroll
-        for (int r = 0; r < RJ; ++r) {
-          Mv[r] = best[r] + ec[r];
-          need[r] = jv[r] && (nextafter(best[r], -INFINITY) + ec[r] == Mv[r]);
-          any_need |= need[r];
-        }
-        if (p.force_slow) {
+          for (int u = 0; u < 16; ++u) S += RED[buf * 16 + u];
+          if (q == 0) {
 #pragma unroll
-          for (int r = 0; r < RJ; ++r) need[r] = jv[r];
-          any_need = true;
-        }
-        if (__any(any_need)) {
-          // rare: an earlier i might tie after adding log e_j -> reference expression
+            for (int r = 0; r < RJN; ++r)
+              if (jv[r]) p.post[(c0 + t) * n + jr[r]] = qv[r] / S;
+          }
+          if (more) {
+            double sc = 1.0;
+            if (rescale) {
+              double M = RED[32 + buf * 16];
 #pragma unroll
-          for (int r = 0; r < RJ; ++r) {
-            if (need[r]) {
-              const double* la = p.mat + jr[r];
-              double bb = (Xb[0] + la[0]) + ec[r];
-              int aa = 0;
-              for (int i = 1; i < n; ++i) {
-                const double v = (Xb[i] + la[(int64_t)i * n]) + ec[r];
-                if (v > bb) {
-                  bb = v;
-                  aa = i;
+              for (int u = 1; u < 16; ++u) M = fmax(M, RED[32 + buf * 16 + u]);
+              if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
+            }
+            double acc[RJN];
+#pragma unroll
+            for (int r = 0; r < RJN; ++r) acc[r] = 0.0;
+            const double* xs = Xb + q * IQS;
+#pragma unroll
+            for (int k = 0; k < IQ; ++k) {
+              const double xi = xs[k];
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) acc[r] = fma(xi, m[k][r], acc[r]);
+            }
+            combine_sum(acc);
+#pragma unroll
+            for (int r = 0; r < RJN; ++r) bt[r] = acc[r] * sc;
+          }
+          buf ^= 1;
+        }
+      } else {
+        // ------------- Viterbi (optimizer.py:305-333), back-pointers as uint8
+        // Back-pointer rows and chunk maps have stride XR: every lane stores (duplicates
+        // store the same byte, padded states a dummy one), no branches.
+        const int o0 = ot.get(0);
+        double x[RJN];
+        int org[RJN];
+#pragma unroll
+        for (int r = 0; r < RJN; ++r) {
+          x[r] = jv[r] ? p.init[o0 * n + jr[r]] : -INFINITY;
+          org[r] = 0;
+        }
+        const int64_t cbase = p.chunk_base[blk];
+        wait_vmem_all();
+        STAMP(-1);
+        for (int t0 = 0; t0 < T; t0 += TE) {
+#pragma unroll
+          for (int sub = 0; sub < TE; ++sub) {
+            const int t = t0 + sub;
+            if (t >= 1 && t < T) {
+              DIAG_STEP();
+              const int buf = sub & 1;  // t0 is even
+              double* Xb = X + buf * (XS + 64);
+              uint8_t* Ob = ORIG + buf * (256 + 64);
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) {
+                Xb[jx[r]] = x[r];
+                Ob[jo[r]] = (uint8_t)org[r];
+              }
+              double ec[RJN];
+              if (sub != 0) {
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) ec[r] = staged(EST, t, jr[r]);
+              }
+              if (sub == 0) {
+                ot.advance(t, tid);
+                stage_commit(t);
+              }
+              STAMP(0);
+              lds_barrier();
+              STAMP(1);
+              if (sub == 0) {
+                stage_issue(t);
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) ec[r] = staged(EST, t, jr[r]);
+              }
+              const double* xs = Xb + q * IQS;
+              // NCH independent first-max chains per target (k = c mod NCH, ascending),
+              // then merged: max value, and the smallest index among the chains holding it.
+              // Every candidate is the reference's exact value (omega_i + log a_ij) + log e_j
+              // (optimizer.py:326-330), so the first maximum is the reference's argmax.
+              double bc[NCH][RJN];
+              int ac[NCH][RJN];
+#pragma unroll
+              for (int c = 0; c < NCH; ++c) {
+                const double xc = xs[c];
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) {
+                  bc[c][r] = (xc + m[c][r]) + ec[r];
+                  ac[c][r] = c;
                 }
               }
-              arg[r] = aa;
+#pragma unroll
+              for (int k = NCH; k < IQ; ++k) {
+                const double xi = xs[k];
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) {
+                  const double y = (xi + m[k][r]) + ec[r];
+                  const bool gt = y > bc[k % NCH][r];
+                  bc[k % NCH][r] = fmax(bc[k % NCH][r], y);
+                  ac[k % NCH][r] = gt ? k : ac[k % NCH][r];
+                }
+              }
+              double best[RJN];
+              int arg[RJN];
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) {
+                double b = bc[0][r];
+#pragma unroll
+                for (int c = 1; c < NCH; ++c) b = fmax(b, bc[c][r]);
+                int a = 0x7fffffff;
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) a = (bc[c][r] == b) ? min(a, ac[c][r]) : a;
+                best[r] = b;
+                arg[r] = a + q * IQ;
+              }
+              STAMP(2);
+              // combine the 8 i-ranges; on equal maxima the lower range (lower i) wins
+              combine_first_max(best, arg);
+              STAMP(3);
+              STAMP(4);
+              // chunk origin tracking: org = state at column (chunk start - 1) on the best
+              // path (VIT_CHUNK is a multiple of TE, so chunk boundaries fall on sub == 0)
+              const bool chunk_start = sub == 0 && (t % VIT_CHUNK) == 0;
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) org[r] = chunk_start ? arg[r] : (int)Ob[arg[r]];
+              uint8_t* bprow = p.bp + (c0 + t) * XR;
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) bprow[jr[r]] = (uint8_t)arg[r];
+              if (sub == TE - 1 || t == T - 1) {
+                const bool chunk_end = ((t + 1) % VIT_CHUNK) == 0 || t == T - 1;
+                if (chunk_end && t >= VIT_CHUNK) {
+                  uint8_t* cm = p.chunk_map + (cbase + t / VIT_CHUNK) * XR;
+#pragma unroll
+                  for (int r = 0; r < RJN; ++r) cm[jr[r]] = (uint8_t)org[r];
+                }
+              }
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) x[r] = jv[r] ? best[r] : -INFINITY;
+              STAMP(5);
             }
           }
         }
-        // chunk origin tracking: org = state at column (chunk start - 1) on the best path
-        const int tc = t % VIT_CHUNK;
+        // last state = first argmax of omega_{T-1}  (optimizer.py:346)
+        double bv = jv[0] ? x[0] : -INFINITY;
+        int bj = jv[0] ? jr[0] : 0x7fffffff;
 #pragma unroll
-        for (int r = 0; r < RJ; ++r) org[r] = (tc == 0) ? arg[r] : (int)Ob[arg[r]];
-        if (q == 0) {
-          const bool chunk_end = (tc == VIT_CHUNK - 1) || (t == T - 1);
+        for (int r = 1; r < RJN; ++r) {
+          if (jv[r] && (x[r] > bv || (x[r] == bv && jr[r] < bj))) {
+            bv = x[r];
+            bj = jr[r];
+          }
+        }
+        wave_first_max(bv, bj);
+        if (l == 0) {
+          RED[32 + w] = bv;
+          REDI[w] = bj;
+        }
+        lds_barrier();
+        if (tid == 0) {
+          double b = RED[32];
+          int a = REDI[0];
 #pragma unroll
-          for (int r = 0; r < RJ; ++r) {
-            if (jv[r]) {
-              p.bp[(c0 + t) * n + jr[r]] = (uint8_t)arg[r];
-              if (chunk_end && t >= VIT_CHUNK)
-                p.chunk_map[(cbase + t / VIT_CHUNK) * n + jr[r]] = (uint8_t)org[r];
+          for (int v = 1; v < W; ++v) {
+            const double c = RED[32 + v];
+            if (c > b) {
+              b = c;
+              a = REDI[v];
             }
           }
-        }
-#pragma unroll
-        for (int r = 0; r < RJ; ++r) x[r] = jv[r] ? Mv[r] : -INFINITY;
-        buf ^= 1;
-      }
-      // last state = first argmax of omega_{T-1}  (optimizer.py:346)
-      double bv = jv[0] ? x[0] : -INFINITY;
-      int bj = jv[0] ? jr[0] : 0x7fffffff;
-#pragma unroll
-      for (int r = 1; r < RJ; ++r) {
-        if (jv[r] && (x[r] > bv || (x[r] == bv && jr[r] < bj))) {
-          bv = x[r];
-          bj = jr[r];
+          p.last_state[blk] = (uint8_t)a;
         }
       }
-      wave_first_max(bv, bj);
-      if (l == 0) {
-        RED[buf * 16 + w] = bv;
-        REDI[w] = bj;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        double b = RED[buf * 16];
-        int a = REDI[0];
-        for (int v = 1; v < W; ++v) {
-          const double c = RED[buf * 16 + v];
-          if (c > b) {
-            b = c;
-            a = REDI[v];
-          }
-        }
-        p.last_state[blk] = (uint8_t)a;
-      }
-    }
-    __syncthreads();
+      if (urgent) __builtin_amdgcn_s_setprio(0);
+    }  // T > 0
+    lds_barrier();
   }
+  DIAG_FLUSH();
 }
 
 // ---------------------------------------------------------------------------------------
@@ -566,7 +706,7 @@ __global__ void __launch_bounds__(MaxBlock<IQ>::value) sweep_kernel(SweepArgs p)
 //          end state (ceil(T/C) hops);
 //   fill:  per chunk, chase the back-pointers from its end state (<= C hops).
 // ---------------------------------------------------------------------------------------
-__global__ void vit_chain_kernel(int n, int64_t nblocks, const int64_t* __restrict__ off,
+__global__ void vit_chain_kernel(int xr, int64_t nblocks, const int64_t* __restrict__ off,
                                  const int64_t* __restrict__ chunk_base,
                                  const uint8_t* __restrict__ chunk_map,
                                  const uint8_t* __restrict__ last_state,
@@ -580,12 +720,12 @@ __global__ void vit_chain_kernel(int n, int64_t nblocks, const int64_t* __restri
   int s = last_state[blk];
   chunk_end[cb + K - 1] = (uint8_t)s;
   for (int64_t k = K - 1; k >= 1; --k) {
-    s = chunk_map[(cb + k) * n + s];
+    s = chunk_map[(cb + k) * xr + s];
     chunk_end[cb + k - 1] = (uint8_t)s;
   }
 }
 
-__global__ void vit_fill_kernel(int n, int64_t nchunks, const int64_t* __restrict__ off,
+__global__ void vit_fill_kernel(int xr, int64_t nchunks, const int64_t* __restrict__ off,
                                 const int64_t* __restrict__ chunk_base,
                                 const int32_t* __restrict__ chunk_blk,
                                 const uint8_t* __restrict__ chunk_end,
@@ -601,96 +741,103 @@ __global__ void vit_fill_kernel(int n, int64_t nchunks, const int64_t* __restric
   int s = chunk_end[c];
   path[c0 + hi - 1] = (uint8_t)s;
   for (int64_t t = hi - 1; t > lo; --t) {
-    s = bp[(c0 + t) * n + s];
+    s = bp[(c0 + t) * xr + s];
     path[c0 + t - 1] = (uint8_t)s;
   }
 }
 
 // ---------------------------------------------------------------------------------------
-// launch helpers
+// launch helpers: (RJN, IQ) configurations by state count
 // ---------------------------------------------------------------------------------------
-static int pick_iq(int n) {
-  const int need = (n + Q - 1) / Q;
-  const int menu[] = {4, 9, 12, 17, 24};
-  for (int v : menu)
-    if (v >= need) return v;
+struct Cfg {
+  int rj, iq;
+};
+static constexpr Cfg kCfgs[] = {{1, 4}, {2, 8}, {3, 9}, {3, 12}, {4, 16}, {5, 17}, {6, 24}};
+
+static int pick_cfg(int n) {
+  for (int c = 0; c < (int)(sizeof kCfgs / sizeof kCfgs[0]); ++c)
+    if (32 * kCfgs[c].rj >= n && Q * kCfgs[c].iq >= n) return c;
   return -1;
 }
 
-size_t sweep_lds_bytes(int xp, int tb) {
-  return (size_t)2 * xp * sizeof(double) + 64 * sizeof(double) + 20 * sizeof(int) +
-         (size_t)2 * tb * sizeof(uint16_t) + (size_t)2 * xp + 64;
+static size_t lds_bytes(int cfg, int mode) {
+  const int iq = kCfgs[cfg].iq, rj = kCfgs[cfg].rj;
+  const int xs = Q * (iq + (iq & 1));
+  const int xr = 32 * rj;
+  const int stages = (mode == MODE_BWD) ? 2 : 1;
+  return (size_t)2 * (xs + 64) * sizeof(double) + 64 * sizeof(double) +
+         (size_t)stages * 2 * TE * xr * sizeof(double) + 32 * sizeof(int) +
+         (size_t)2 * TB * sizeof(uint16_t) + 2 * (256 + 64);
 }
 
-template <int IQ, int MODE>
-static hipError_t launch_iq(const SweepArgs& a, int grid, int block, size_t lds,
-                            hipStream_t st) {
-  hipLaunchKernelGGL((sweep_kernel<IQ, MODE>), dim3(grid), dim3(block), lds, st, a);
+template <int RJN, int IQ, int MODE>
+static hipError_t launch_one(const SweepArgs& a, int grid, size_t lds, hipStream_t st) {
+  hipLaunchKernelGGL((sweep_kernel<RJN, IQ, MODE>), dim3(grid), dim3(TB), lds, st, a);
   return hipGetLastError();
 }
-
-template <int MODE>
-static hipError_t launch_mode(int iq, const SweepArgs& a, int grid, int block, size_t lds,
-                              hipStream_t st) {
-  switch (iq) {
-    case 4: return launch_iq<4, MODE>(a, grid, block, lds, st);
-    case 9: return launch_iq<9, MODE>(a, grid, block, lds, st);
-    case 12: return launch_iq<12, MODE>(a, grid, block, lds, st);
-    case 17: return launch_iq<17, MODE>(a, grid, block, lds, st);
-    case 24: return launch_iq<24, MODE>(a, grid, block, lds, st);
-  }
-  return hipErrorInvalidValue;
-}
-
-template <int IQ, int MODE>
-static int occ_iq(int block, size_t lds) {
+template <int RJN, int IQ, int MODE>
+static int occ_one(size_t lds) {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweep_kernel<IQ, MODE>, block, lds) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweep_kernel<RJN, IQ, MODE>, TB, lds) !=
       hipSuccess)
     return 1;
   return nb > 0 ? nb : 1;
 }
+
 template <int MODE>
-static int occ_mode(int iq, int block, size_t lds) {
-  switch (iq) {
-    case 4: return occ_iq<4, MODE>(block, lds);
-    case 9: return occ_iq<9, MODE>(block, lds);
-    case 12: return occ_iq<12, MODE>(block, lds);
-    case 17: return occ_iq<17, MODE>(block, lds);
-    case 24: return occ_iq<24, MODE>(block, lds);
+static hipError_t dispatch(int cfg, bool launch, const SweepArgs* a, int grid, size_t lds,
+                           hipStream_t st, int* occ) {
+#define ITR_CFG(C, RJN, IQ)                                          \
+  case C:                                                            \
+    if (launch) return launch_one<RJN, IQ, MODE>(*a, grid, lds, st); \
+    *occ = occ_one<RJN, IQ, MODE>(lds);                              \
+    return hipSuccess;
+  switch (cfg) {
+    ITR_CFG(0, 1, 4)
+    ITR_CFG(1, 2, 8)
+    ITR_CFG(2, 3, 9)
+    ITR_CFG(3, 3, 12)
+    ITR_CFG(4, 4, 16)
+    ITR_CFG(5, 5, 17)
+    ITR_CFG(6, 6, 24)
   }
-  return 1;
+#undef ITR_CFG
+  return hipErrorInvalidValue;
+}
+
+static hipError_t dispatch_mode(int mode, int cfg, bool launch, const SweepArgs* a, int grid,
+                                size_t lds, hipStream_t st, int* occ) {
+  switch (mode) {
+    case MODE_FWD_LL: return dispatch<MODE_FWD_LL>(cfg, launch, a, grid, lds, st, occ);
+    case MODE_FWD_STORE: return dispatch<MODE_FWD_STORE>(cfg, launch, a, grid, lds, st, occ);
+    case MODE_BWD: return dispatch<MODE_BWD>(cfg, launch, a, grid, lds, st, occ);
+    case MODE_VIT: return dispatch<MODE_VIT>(cfg, launch, a, grid, lds, st, occ);
+  }
+  return hipErrorInvalidValue;
 }
 
 SweepGeometry sweep_geometry(int n, int mode) {
   SweepGeometry g{};
-  g.iq = pick_iq(n);
-  const int waves = (n + JW - 1) / JW;
-  g.block = waves * 64;
-  g.xp = waves * JW;
-  if (Q * g.iq > g.xp) g.xp = Q * g.iq;
-  g.xp = (g.xp + 15) & ~15;
-  g.lds = sweep_lds_bytes(g.xp, g.block);
+  g.iq = pick_cfg(n);  // configuration index (negative: unsupported)
+  g.block = TB;
+  g.xp = 0;
+  if (g.iq < 0) return g;
+  g.lds = lds_bytes(g.iq, mode);
   int occ = 1;
-  switch (mode) {
-    case MODE_FWD_LL: occ = occ_mode<MODE_FWD_LL>(g.iq, g.block, g.lds); break;
-    case MODE_FWD_STORE: occ = occ_mode<MODE_FWD_STORE>(g.iq, g.block, g.lds); break;
-    case MODE_BWD: occ = occ_mode<MODE_BWD>(g.iq, g.block, g.lds); break;
-    case MODE_VIT: occ = occ_mode<MODE_VIT>(g.iq, g.block, g.lds); break;
-  }
+  (void)dispatch_mode(mode, g.iq, false, nullptr, 0, g.lds, nullptr, &occ);
   g.per_cu = occ;
   return g;
 }
 
 hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepArgs& a,
                         hipStream_t st) {
-  switch (mode) {
-    case MODE_FWD_LL: return launch_mode<MODE_FWD_LL>(g.iq, a, grid, g.block, g.lds, st);
-    case MODE_FWD_STORE: return launch_mode<MODE_FWD_STORE>(g.iq, a, grid, g.block, g.lds, st);
-    case MODE_BWD: return launch_mode<MODE_BWD>(g.iq, a, grid, g.block, g.lds, st);
-    case MODE_VIT: return launch_mode<MODE_VIT>(g.iq, a, grid, g.block, g.lds, st);
-  }
-  return hipErrorInvalidValue;
+  int occ = 0;
+  return dispatch_mode(mode, g.iq, true, &a, grid, g.lds, st, &occ);
+}
+
+int sweep_row_stride(int n) {  // padded target states: row stride of bp / alpha rows
+  const int c = pick_cfg(n);
+  return c < 0 ? -1 : 32 * kCfgs[c].rj;
 }
 
 hipError_t launch_vit_traceback(int n, int64_t nblocks, int64_t nchunks, const int64_t* off,
@@ -701,14 +848,16 @@ hipError_t launch_vit_traceback(int n, int64_t nblocks, int64_t nchunks, const i
   if (nblocks > 0) {
     const int tb = 256;
     hipLaunchKernelGGL(vit_chain_kernel, dim3((unsigned)((nblocks + tb - 1) / tb)), dim3(tb),
-                       0, st, n, nblocks, off, chunk_base, chunk_map, last_state, chunk_end);
+                       0, st, sweep_row_stride(n), nblocks, off, chunk_base, chunk_map, last_state,
+                       chunk_end);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   if (nchunks > 0) {
     const int tb = 256;
     hipLaunchKernelGGL(vit_fill_kernel, dim3((unsigned)((nchunks + tb - 1) / tb)), dim3(tb), 0,
-                       st, n, nchunks, off, chunk_base, chunk_blk, chunk_end, bp, path);
+                       st, sweep_row_stride(n), nchunks, off, chunk_base, chunk_blk, chunk_end, bp,
+                       path);
     return hipGetLastError();
   }
   return hipSuccess;

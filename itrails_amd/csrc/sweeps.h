@@ -23,17 +23,18 @@ struct SweepArgs {
   const double* emit;           // E or log E, 625 x n
   const double* init;           // pi*E or log(pi*E), 625 x n
   double* loglik;               // [nblocks]                       (MODE_FWD_LL)
-  double* alpha;                // [total x n] rescaled forward rows (FWD_STORE out, BWD in)
+  double* alpha;                // [total x XR] rescaled forward rows (FWD_STORE out, BWD in)
   double* post;                 // [total x n] posteriors          (MODE_BWD)
-  uint8_t* bp;                  // [total x n] back-pointers       (MODE_VIT)
-  uint8_t* chunk_map;           // [nchunks x n] chunk origin maps (MODE_VIT)
+  uint8_t* bp;                  // [total x XR] back-pointers      (MODE_VIT)
+  uint8_t* chunk_map;           // [nchunks x XR] chunk origin maps (MODE_VIT)
   const int64_t* chunk_base;    // [nblocks] first chunk of each block
   uint8_t* last_state;          // [nblocks] argmax of the last column (MODE_VIT)
-  int force_slow;               // test hook: take the Viterbi tie re-scan for every state
+  int prio_len;                 // blocks at least this long run at raised wave priority
+  uint64_t* diag;               // diagnostic build only: per-segment cycle sums
 };
 
 struct SweepGeometry {
-  int iq;       // source states per lane (template)
+  int iq;       // kernel configuration index (negative: unsupported)
   int block;    // threads per workgroup (64 * waves)
   int xp;       // padded vector length
   size_t lds;   // dynamic LDS bytes
@@ -41,6 +42,7 @@ struct SweepGeometry {
 };
 
 SweepGeometry sweep_geometry(int n, int mode);
+int sweep_row_stride(int n);  // row stride (padded states) of back-pointer / forward rows
 hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepArgs& a,
                         hipStream_t st);
 hipError_t launch_vit_traceback(int n, int64_t nblocks, int64_t nchunks, const int64_t* off,

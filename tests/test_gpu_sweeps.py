@@ -84,22 +84,6 @@ def test_ties_first_maximum(gpu):
     np.testing.assert_array_equal(hmm._paths(model, plan, obs), O.viterbi(t, obs, off))
 
 
-def test_tie_rescan_path_is_exact(gpu, monkeypatch):
-    """The kernel skips the `+ log e_j` add and re-scans a state only when it cannot prove
-    the argmax unchanged; forcing the re-scan for every state must give the same paths."""
-    rng = np.random.default_rng(11)
-    a, b, pi = random_hmm(rng, 70)
-    obs, off, _ = sample_alignment(a, b, pi, [3000, 1, 2000, 600], seed=4)
-    model = hmm.Model(a, b, pi)
-    fast = hmm._paths(model, hmm.Plan(off), obs)
-    monkeypatch.setenv("ITR_FORCE_SLOW_TIES", "1")
-    slow = hmm._paths(model, hmm.Plan(off), obs)
-    monkeypatch.delenv("ITR_FORCE_SLOW_TIES")
-    hmm.Plan(off)  # resets the hook
-    np.testing.assert_array_equal(fast, slow)
-    np.testing.assert_array_equal(fast, O.viterbi(build_tables(a, b, pi), obs, off))
-
-
 @pytest.mark.parametrize("name", [m for m in model_fixtures() if m != "model_kat_1_1.npz"])
 def test_reference_models_vs_oracle(gpu, name):
     """The reference's own model builds (a, b, pi from trans_emiss_calc) on sampled data."""
