@@ -6,8 +6,9 @@
 // ------------------
 // A MAF block is a strictly sequential recurrence over its columns: the only parallelism
 // inside a block is the N x N state contraction of one column step, and the longest block
-// bounds the makespan.  One WORKGROUP of exactly four wavefronts — one per SIMD of the CU,
-// so the per-step VALU issue is balanced — owns one block at a time.  Blocks are pulled
+// bounds the makespan.  One WORKGROUP of W = ceil(N/8) wavefronts (one target state per
+// lane: 2-3 waves interleave on each SIMD, and a lone wave would issue FP64 at only about
+// half the SIMD's rate) owns one block at a time.  Blocks are pulled
 // longest-first from a device work queue, and the longest ones run at raised wave priority
 // (s_setprio) against the co-resident workgroups that work through the short ones.
 //
@@ -36,6 +37,7 @@
 // then + log e_j, IEEE adds only, first maximum wins — so paths are bit-identical for
 // identical tables.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <math.h>
 #include <stdint.h>
 
@@ -43,8 +45,6 @@
 
 namespace itr {
 
-static constexpr int W = 4;        // wavefronts per workgroup: one per SIMD
-static constexpr int TB = 64 * W;  // threads per workgroup
 static constexpr int Q = 8;        // lanes splitting the i-sum of one target state
 static constexpr int TE = 16;      // columns per staged tile of per-column rows
 static constexpr double LN2 = 0.69314718055994530942;
@@ -174,14 +174,15 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// Observed symbols of the current block staged in LDS, 256 steps per tile (forward: step s
-// is column s; backward: column T-1-s).  Two tiles are resident and the next one is in
-// flight in a register of every thread, so its global load is waited for 256 steps after
-// it was issued.
+// Observed symbols of the current block staged in LDS, one per thread per tile (forward:
+// step s is column s; backward: column T-1-s).  Two tiles are resident and the next one is
+// in flight in a register of every thread, so its global load is waited for a whole tile
+// after it was issued.
 struct ObsTiles {
-  uint16_t* lds;      // [2][TB]
+  uint16_t* lds;      // [2][tb]
   const uint16_t* g;  // block's first column
   int T, dir;         // dir = +1 forward, -1 backward
+  int tb;             // symbols per tile = threads per workgroup
   int inflight;       // this thread's element of the next tile to store
 
   __device__ __forceinline__ int col(int s) const { return dir > 0 ? s : T - 1 - s; }
@@ -193,20 +194,20 @@ struct ObsTiles {
   __device__ __forceinline__ static uint16_t clamp(int v) { return (uint16_t)min(v, 624); }
   __device__ __forceinline__ void start(int tid) {  // tiles 0, 1 in LDS; tile 2 in flight
     lds[tid] = clamp(fetch(tid));
-    lds[TB + tid] = clamp(fetch(TB + tid));
-    inflight = fetch(2 * TB + tid);
+    lds[tb + tid] = clamp(fetch(tb + tid));
+    inflight = fetch(2 * tb + tid);
   }
   // at step s (before the step's barrier): when s starts tile k >= 1, tile k+1 replaces
   // tile k-1 and tile k+2 is requested
   __device__ __forceinline__ void advance(int s, int tid) {
-    if (s >= TB && (s & (TB - 1)) == 0) {
-      const int k = s / TB;
-      lds[((k + 1) & 1) * TB + tid] = clamp(inflight);
-      inflight = fetch((k + 2) * TB + tid);
+    if (s >= tb && (s % tb) == 0) {
+      const int k = s / tb;
+      lds[((k + 1) & 1) * tb + tid] = clamp(inflight);
+      inflight = fetch((k + 2) * tb + tid);
     }
   }
   __device__ __forceinline__ int get(int s) const {  // symbol at step s (LDS broadcast)
-    return (s < T) ? (int)lds[((s / TB) & 1) * TB + (s & (TB - 1))] : 0;
+    return (s < T) ? (int)lds[((s / tb) & 1) * tb + (s % tb)] : 0;
   }
 };
 
@@ -214,10 +215,12 @@ struct ObsTiles {
 // column) for TE consecutive steps, loaded into registers one tile ahead and committed to an
 // LDS ring [2][TE][XR] at the tile boundary.  Element idx = tid + e*TB of a tile is row
 // idx / XR, target state idx % XR.
-template <int RJN>
+template <int WV, int RJN>
 struct RowStage {
-  static constexpr int XR = 32 * RJN;      // padded target states
+  static constexpr int TB = 64 * WV;
+  static constexpr int XR = WV * 8 * RJN;  // padded target states
   static constexpr int RS = TE * XR / TB;  // = 2 * RJN elements per thread
+  static_assert(RS * TB == TE * XR, "tile must split evenly over the workgroup");
   double v[RS];
   template <class RowOf>
   __device__ __forceinline__ void issue(const double* __restrict__ g, int stride, int ncol,
@@ -239,15 +242,27 @@ struct RowStage {
 // ---------------------------------------------------------------------------------------
 // the sweep kernel: RJN target states per lane, IQ source states per lane
 // ---------------------------------------------------------------------------------------
-// co-resident workgroups per CU the register budget is sized for (one wave per SIMD each)
-template <int RJN, int IQ, int MODE>
+// co-resident workgroups per CU the register budget is sized for
+template <int WV, int RJN, int IQ, int MODE>
 struct Occ {
-  static constexpr int base = RJN * IQ <= 27 ? 3 : RJN * IQ <= 64 ? 2 : 1;
-  static constexpr int value = (MODE == MODE_BWD && base > 1) ? base - 1 : base;
+  // VGPRs a lane needs: its slice of the matrix, the source values it reads, working set
+  static constexpr int need = 2 * RJN * IQ + 2 * IQ + 64;
+  static constexpr int simd_waves = 512 / need;  // waves one SIMD's register file holds
+  static constexpr int fit = simd_waves * 4 / WV;
+  static constexpr int wide = fit > 3 ? 3 : (fit < 1 ? 1 : fit);
+  // four-wave configurations: budget measured on the (5,5) model (N = 70)
+  static constexpr int narrow = RJN * IQ <= 27 ? 3 : RJN * IQ <= 64 ? 2 : 1;
+  static constexpr int base = WV == 4 ? narrow : wide;
+  static constexpr int wgs = (MODE == MODE_BWD && base > 1) ? base - 1 : base;
+  // launch_bounds' second argument is waves per SIMD: WGs per CU x waves per WG / 4
+  static constexpr int value = (wgs * WV + 3) / 4;
 };
 
-template <int RJN, int IQ, int MODE>
-__global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(SweepArgs p) {
+template <int WV, int RJN, int IQ, int MODE>
+__global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
+    sweep_kernel(SweepArgs p) {
+  constexpr int W = WV;       // wavefronts per workgroup
+  constexpr int TB = 64 * W;  // threads per workgroup
   constexpr int IQS = IQ + (IQ & 1);  // 16-byte aligned source ranges in LDS
   constexpr int XS = Q * IQS;         // published vector length
   constexpr int JW = 8 * RJN;         // target states per wave
@@ -260,16 +275,17 @@ __global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(
   const int l = tid & 63;
   const int q = l & (Q - 1);
   const int jl = l >> 3;
-  const int row16 = w * 4 + (l >> 4);  // 16-lane row of the workgroup (0..15)
+  const int row16 = w * 4 + (l >> 4);  // 16-lane row of the workgroup (0..4W-1)
+  constexpr int NROW = 4 * W;
   const bool row_leader = (l & 15) == 0;
 
   double* X = reinterpret_cast<double*>(smem);  // [2][XS+64]    published vectors + a
                                                 //               per-lane write sink
-  double* RED = X + 2 * (XS + 64);              // [4][16]       row partials
-  double* EST = RED + 64;                       // [2][TE][XR]   staged emission rows
+  double* RED = X + 2 * (XS + 64);              // [5][64]       row partials
+  double* EST = RED + 5 * 64;                   // [2][TE][XR]   staged emission rows
   double* AST = EST + 2 * TE * XR;              // [2][TE][XR]   staged forward rows (BWD)
   int* SBLK = reinterpret_cast<int*>(AST + ((MODE == MODE_BWD) ? 2 * TE * XR : 0));
-  int* REDI = SBLK + 4;                                      // [4]
+  int* REDI = SBLK + 4;                                      // [16]
   uint16_t* OBS = reinterpret_cast<uint16_t*>(SBLK + 32);    // [2][TB]
   uint8_t* ORIG = reinterpret_cast<uint8_t*>(OBS + 2 * TB);  // [2][256+64] (Viterbi)
 
@@ -302,8 +318,8 @@ __global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(
   for (int i = tid; i < 2 * (XS + 64); i += TB) X[i] = pad;
   lds_barrier();
 
-  RowStage<RJN> est;
-  RowStage<RJN> ast;
+  RowStage<W, RJN> est;
+  RowStage<W, RJN> ast;
   (void)ast;
   DIAG_DECL
 
@@ -324,7 +340,7 @@ __global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(
     } else {
       const bool urgent = T >= p.prio_len;
       if (urgent) __builtin_amdgcn_s_setprio(2);
-      ObsTiles ot{OBS, p.obs + c0, T, (MODE == MODE_BWD) ? -1 : +1, 0};
+      ObsTiles ot{OBS, p.obs + c0, T, (MODE == MODE_BWD) ? -1 : +1, TB, 0};
       ot.start(tid);
       lds_barrier();
       auto sym_row = [&](int s) -> int64_t { return s < T ? (int64_t)ot.get(s) : -1; };
@@ -390,7 +406,7 @@ __global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(
 #pragma unroll
                 for (int r = 1; r < RJN; ++r) mx = fmax(mx, x[r]);
                 mx = fmax(mx, dpp_f64<DPP_R8>(mx));
-                if (row_leader) RED[buf * 16 + row16] = mx;
+                if (row_leader) RED[128 + buf * 64 + row16] = mx;
               }
               // emission factors of column t: staged at the start of this tile, so (except
               // on the tile's first step, which commits them) readable before the barrier
@@ -426,9 +442,9 @@ __global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(
                 for (int r = 0; r < RJN; ++r) acc[k % NCH][r] = fma(xi, m[k][r], acc[k % NCH][r]);
               }
               if (rescale) {  // fold 2^-e into the emission factor (off the FMA chain)
-                double M = RED[buf * 16];
+                double M = RED[128 + buf * 64];
 #pragma unroll
-                for (int v = 1; v < 16; ++v) M = fmax(M, RED[buf * 16 + v]);
+                for (int v = 1; v < NROW; ++v) M = fmax(M, RED[128 + buf * 64 + v]);
                 const bool ok = M > 0.0 && M < INFINITY;
                 const int e = ok ? ilogb(M) : 0;
                 const double sc = ldexp(1.0, -e);
@@ -465,12 +481,12 @@ __global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(
             for (int r = 0; r < RJN; ++r) part += jv[r] ? x[r] : 0.0;
           }
           part = wave_sum(part);
-          if (l == 0) RED[32 + w] = part;
+          if (l == 0) RED[256 + w] = part;
           lds_barrier();
           if (tid == 0) {
             double tot = 0.0;
 #pragma unroll
-            for (int v = 0; v < W; ++v) tot += RED[32 + v];
+            for (int v = 0; v < W; ++v) tot += RED[256 + v];
             p.loglik[blk] = log(tot) + (double)K * LN2;
           }
         }
@@ -498,7 +514,7 @@ __global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(
             ps += qv[r];
           }
           ps += dpp_f64<DPP_R8>(ps);  // the row's two target-state groups
-          if (row_leader) RED[buf * 16 + row16] = ps;
+          if (row_leader) RED[buf * 64 + row16] = ps;
           double* Xb = X + buf * (XS + 64);
           const bool more = t > 0;
           const bool rescale = (s & 7) == 0;
@@ -513,13 +529,13 @@ __global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(
 #pragma unroll
               for (int r = 1; r < RJN; ++r) mx = fmax(mx, v[r]);
               mx = fmax(mx, dpp_f64<DPP_R8>(mx));
-              if (row_leader) RED[32 + buf * 16 + row16] = mx;
+              if (row_leader) RED[128 + buf * 64 + row16] = mx;
             }
           }
           lds_barrier();
           double S = 0.0;
 #pragma unroll
-          for (int u = 0; u < 16; ++u) S += RED[buf * 16 + u];
+          for (int u = 0; u < NROW; ++u) S += RED[buf * 64 + u];
           if (q == 0) {
 #pragma unroll
             for (int r = 0; r < RJN; ++r)
@@ -528,9 +544,9 @@ __global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(
           if (more) {
             double sc = 1.0;
             if (rescale) {
-              double M = RED[32 + buf * 16];
+              double M = RED[128 + buf * 64];
 #pragma unroll
-              for (int u = 1; u < 16; ++u) M = fmax(M, RED[32 + buf * 16 + u]);
+              for (int u = 1; u < NROW; ++u) M = fmax(M, RED[128 + buf * 64 + u]);
               if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
             }
             double acc[RJN];
@@ -674,16 +690,16 @@ __global__ void __launch_bounds__(TB, (Occ<RJN, IQ, MODE>::value)) sweep_kernel(
         }
         wave_first_max(bv, bj);
         if (l == 0) {
-          RED[32 + w] = bv;
+          RED[256 + w] = bv;
           REDI[w] = bj;
         }
         lds_barrier();
         if (tid == 0) {
-          double b = RED[32];
+          double b = RED[256];
           int a = REDI[0];
 #pragma unroll
           for (int v = 1; v < W; ++v) {
-            const double c = RED[32 + v];
+            const double c = RED[256 + v];
             if (c > b) {
               b = c;
               a = REDI[v];
@@ -750,36 +766,54 @@ __global__ void vit_fill_kernel(int xr, int64_t nchunks, const int64_t* __restri
 // launch helpers: (RJN, IQ) configurations by state count
 // ---------------------------------------------------------------------------------------
 struct Cfg {
-  int rj, iq;
+  int w, rj, iq;  // waves, target states per lane, source states per lane
 };
-static constexpr Cfg kCfgs[] = {{1, 4}, {2, 8}, {3, 9}, {3, 12}, {4, 16}, {5, 17}, {6, 24}};
+// one target state per lane wherever the workgroup fits in 16 waves: more waves interleave
+// on each SIMD (a lone wave issues FP64 at about half the SIMD's rate) and the slots pad N
+// by at most 7
+static constexpr Cfg kCfgs[] = {
+    // four waves (one per SIMD), several targets per lane: best throughput per CU (several
+    // workgroups co-resident); chosen automatically
+    {4, 1, 4}, {4, 2, 8}, {4, 3, 9}, {4, 3, 12}, {4, 4, 16}, {4, 5, 17}, {4, 6, 24},
+    // one target per lane, W = ceil(N/8) waves: ~25% lower step latency for a single long
+    // block but one workgroup per CU (experiments: ITR_SWEEP_CFG=7..13)
+    {4, 1, 4}, {8, 1, 8}, {9, 1, 9}, {12, 1, 12}, {16, 1, 16}, {9, 2, 17}, {8, 3, 24}};
+static constexpr int kAutoCfgs = 7;  // entries pick_cfg chooses from
 
 static int pick_cfg(int n) {
-  for (int c = 0; c < (int)(sizeof kCfgs / sizeof kCfgs[0]); ++c)
-    if (32 * kCfgs[c].rj >= n && Q * kCfgs[c].iq >= n) return c;
+  const char* force = getenv("ITR_SWEEP_CFG");  // experiments: force a configuration
+  if (force) {
+    const int c = atoi(force);
+    if (c >= 0 && c < (int)(sizeof kCfgs / sizeof kCfgs[0]) &&
+        8 * kCfgs[c].w * kCfgs[c].rj >= n && Q * kCfgs[c].iq >= n)
+      return c;
+  }
+  for (int c = 0; c < kAutoCfgs; ++c)
+    if (8 * kCfgs[c].w * kCfgs[c].rj >= n && Q * kCfgs[c].iq >= n) return c;
   return -1;
 }
 
 static size_t lds_bytes(int cfg, int mode) {
-  const int iq = kCfgs[cfg].iq, rj = kCfgs[cfg].rj;
+  const int w = kCfgs[cfg].w, iq = kCfgs[cfg].iq, rj = kCfgs[cfg].rj;
   const int xs = Q * (iq + (iq & 1));
-  const int xr = 32 * rj;
+  const int xr = 8 * w * rj;
+  const int tb = 64 * w;
   const int stages = (mode == MODE_BWD) ? 2 : 1;
-  return (size_t)2 * (xs + 64) * sizeof(double) + 64 * sizeof(double) +
+  return (size_t)2 * (xs + 64) * sizeof(double) + 5 * 64 * sizeof(double) +
          (size_t)stages * 2 * TE * xr * sizeof(double) + 32 * sizeof(int) +
-         (size_t)2 * TB * sizeof(uint16_t) + 2 * (256 + 64);
+         (size_t)2 * tb * sizeof(uint16_t) + 2 * (256 + 64);
 }
 
-template <int RJN, int IQ, int MODE>
+template <int WV, int RJN, int IQ, int MODE>
 static hipError_t launch_one(const SweepArgs& a, int grid, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((sweep_kernel<RJN, IQ, MODE>), dim3(grid), dim3(TB), lds, st, a);
+  hipLaunchKernelGGL((sweep_kernel<WV, RJN, IQ, MODE>), dim3(grid), dim3(64 * WV), lds, st, a);
   return hipGetLastError();
 }
-template <int RJN, int IQ, int MODE>
+template <int WV, int RJN, int IQ, int MODE>
 static int occ_one(size_t lds) {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweep_kernel<RJN, IQ, MODE>, TB, lds) !=
-      hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sweep_kernel<WV, RJN, IQ, MODE>,
+                                                   64 * WV, lds) != hipSuccess)
     return 1;
   return nb > 0 ? nb : 1;
 }
@@ -787,19 +821,26 @@ static int occ_one(size_t lds) {
 template <int MODE>
 static hipError_t dispatch(int cfg, bool launch, const SweepArgs* a, int grid, size_t lds,
                            hipStream_t st, int* occ) {
-#define ITR_CFG(C, RJN, IQ)                                          \
-  case C:                                                            \
-    if (launch) return launch_one<RJN, IQ, MODE>(*a, grid, lds, st); \
-    *occ = occ_one<RJN, IQ, MODE>(lds);                              \
+#define ITR_CFG(C, WV, RJN, IQ)                                          \
+  case C:                                                                \
+    if (launch) return launch_one<WV, RJN, IQ, MODE>(*a, grid, lds, st); \
+    *occ = occ_one<WV, RJN, IQ, MODE>(lds);                              \
     return hipSuccess;
   switch (cfg) {
-    ITR_CFG(0, 1, 4)
-    ITR_CFG(1, 2, 8)
-    ITR_CFG(2, 3, 9)
-    ITR_CFG(3, 3, 12)
-    ITR_CFG(4, 4, 16)
-    ITR_CFG(5, 5, 17)
-    ITR_CFG(6, 6, 24)
+    ITR_CFG(0, 4, 1, 4)
+    ITR_CFG(1, 4, 2, 8)
+    ITR_CFG(2, 4, 3, 9)
+    ITR_CFG(3, 4, 3, 12)
+    ITR_CFG(4, 4, 4, 16)
+    ITR_CFG(5, 4, 5, 17)
+    ITR_CFG(6, 4, 6, 24)
+    ITR_CFG(7, 4, 1, 4)
+    ITR_CFG(8, 8, 1, 8)
+    ITR_CFG(9, 9, 1, 9)
+    ITR_CFG(10, 12, 1, 12)
+    ITR_CFG(11, 16, 1, 16)
+    ITR_CFG(12, 9, 2, 17)
+    ITR_CFG(13, 8, 3, 24)
   }
 #undef ITR_CFG
   return hipErrorInvalidValue;
@@ -819,13 +860,15 @@ static hipError_t dispatch_mode(int mode, int cfg, bool launch, const SweepArgs*
 SweepGeometry sweep_geometry(int n, int mode) {
   SweepGeometry g{};
   g.iq = pick_cfg(n);  // configuration index (negative: unsupported)
-  g.block = TB;
   g.xp = 0;
   if (g.iq < 0) return g;
+  g.block = 64 * kCfgs[g.iq].w;
   g.lds = lds_bytes(g.iq, mode);
   int occ = 1;
   (void)dispatch_mode(mode, g.iq, false, nullptr, 0, g.lds, nullptr, &occ);
   g.per_cu = occ;
+  const char* pcu = getenv("ITR_PER_CU");  // experiments: resident workgroups per CU
+  if (pcu && atoi(pcu) > 0) g.per_cu = atoi(pcu);
   return g;
 }
 
@@ -837,7 +880,7 @@ hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepA
 
 int sweep_row_stride(int n) {  // padded target states: row stride of bp / alpha rows
   const int c = pick_cfg(n);
-  return c < 0 ? -1 : 32 * kCfgs[c].rj;
+  return c < 0 ? -1 : 8 * kCfgs[c].w * kCfgs[c].rj;
 }
 
 hipError_t launch_vit_traceback(int n, int64_t nblocks, int64_t nchunks, const int64_t* off,

@@ -15,6 +15,7 @@ torch.cuda.set_device(0)
 model = hmm.Model(a, b, pi)
 names = {"fwd": ["pre-barrier", "barrier", "reads+fma", "combine", "mul", "post"],
          "vit": ["pre-barrier", "barrier", "reads+max", "combine", "tie/M", "post"]}
+tag = os.environ.get("ITR_SWEEP_CFG", "auto") + "/" + os.environ.get("ITR_PER_CU", "api")
 for label, lengths in [("1x20000", [20000]), ("256x20000", [20000] * 256), ("768x5000", [5000] * 768)]:
     obs, off, _ = sample_alignment(a, b, pi, lengths, seed=1)
     plan = hmm.Plan(off)
@@ -30,5 +31,5 @@ for label, lengths in [("1x20000", [20000]), ("256x20000", [20000] * 256), ("768
         tot = sum(per.values())
         T = max(lengths)
         clk = tot * T / (ms * 1e-3) / 1e9  # cycles per step * steps / time
-        print(label, kind, json.dumps({"ms": round(ms, 3), "cycles_per_step": round(tot, 1),
+        print(tag, label, kind, json.dumps({"ms": round(ms, 3), "cycles_per_step": round(tot, 1),
               "implied_GHz": round(clk, 3), **per}), flush=True)
