@@ -129,10 +129,29 @@ ITR_API int itr_last_kernel_ms(const char* which, double* ms);
 
 /* out[b] = expm(A[b]) for b < batch, each n x n row-major float64 (device pointers).
  * Replaces expm (expm.py:9-167): Higham's Pade 3/5/7/9/13 with scaling & squaring, the
- * branch chosen per matrix from its 1-norm exactly as expm.py:16-143. */
+ * branch chosen per matrix from its 1-norm exactly as expm.py:16-143, r = solve(V-U, V+U)
+ * by LU with partial pivoting, then s squarings (np.linalg.matrix_power(r, 2**s)).  Used by
+ * the Van Loan integrals (vanloan.py:392-425: expm of the block matrix, top-right block) and
+ * every interval propagator of the CTMCs (get_joint_prob_mat.py:119-123,
+ * run_markov_chain_AB.py:105-271, run_markov_chain_ABC.py:312-510,
+ * get_emission_prob_mat.py:22-44).  Synchronises `stream` once (branch selection). */
 ITR_API int itr_expm_batched(int n, int64_t batch, const double* d_A, double* d_out,
                              void* stream);
 ITR_API int itr_expm_batched_host(int n, int64_t batch, const double* h_A, double* h_out);
+
+/* Solve M_b X_b = R_b for b < batch (M n x n, R n x nrhs, row-major, contiguous batches).
+ * M is overwritten by its LU factors (partial pivoting, first maximum |.| like LAPACK
+ * idamax), R by X.  Replaces np.linalg.inv in deepest_ti (deepest_ti.py:256: the last n
+ * columns of C^-1 are solve(C, I[:, -n:])). */
+ITR_API int itr_solve_batched(int n, int nrhs, int64_t batch, double* d_M, double* d_R,
+                              void* stream);
+
+/* C_b = alpha * A_b (m x k) @ B_b (k x n) + beta * C_b, contiguous row-major batches
+ * (MFMA f64 16x16x4 tiles).  The contractions of the chain steps (prob @ (mask E mask),
+ * run_markov_chain_ABC.py:9-14; deepest_ti.py:256 product with A_last). */
+ITR_API int itr_gemm_batched(int m, int n, int k, int64_t batch, double alpha,
+                             const double* d_A, const double* d_B, double beta, double* d_C,
+                             void* stream);
 
 #ifdef __cplusplus
 }

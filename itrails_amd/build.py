@@ -8,7 +8,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["hmm_sweeps.hip", "expm.hip", "capi.cpp"]
+SOURCES = ["hmm_sweeps.hip", "dense.hip", "capi.cpp"]
 OUT = os.path.join(HERE, "libitrails_hip.so")
 ARCH = os.environ.get("ITR_OFFLOAD_ARCH", "gfx950")
 
@@ -27,16 +27,27 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
     if not force and not diag and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-fvisibility=hidden"]
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+             "-fvisibility=hidden"]
     if diag:
-        cmd += ["-DITR_DIAG"]
-    cmd += [os.path.join(CSRC, s) for s in SOURCES]
-    cmd += ["-o", out + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
+        flags += ["-DITR_DIAG"]
+    tag = "_diag" if diag else ""
+    objs, procs = [], []
+    for src in SOURCES:  # one compiler per translation unit, in parallel
+        obj = os.path.join(CSRC, "..", f".{os.path.splitext(src)[0]}{tag}.o")
+        cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    rcs = [p.wait() for p in procs]
+    if any(rcs):
+        raise subprocess.CalledProcessError(max(rcs), "hipcc")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", out + ".tmp"]
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
+    for o in objs:
+        os.remove(o)
     return out
 
 

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/itrails_hip.h"
+#include "dense.h"
 #include "sweeps.h"
 
 namespace {
@@ -505,14 +506,9 @@ int itr_expm_batched(int n, int64_t batch, const double* A, double* out, void* s
   if (batch == 0) return 0;
   if (!A || !out) return fail(ITR_EINVAL, "null device pointer");
   hipStream_t st = (hipStream_t)stream;
-  const size_t wb = itr::expm_workspace_bytes(n, batch);
-  DevBuf w;
-  HIP_TRY(hipMallocAsync(&w.p, wb ? wb : 8, st));
   Scope sc("expm", st);
-  hipError_t e = itr::launch_expm_batched(n, batch, A, out, (double*)w.p, st);
-  (void)hipFreeAsync(w.p, st);
-  w.p = nullptr;
-  if (e != hipSuccess) return fail(ITR_EHIP, "expm launch failed: %s", hipGetErrorString(e));
+  const hipError_t e = itr::expm_batched(n, batch, A, out, st);
+  if (e != hipSuccess) return fail(ITR_EHIP, "expm failed: %s", hipGetErrorString(e));
   return 0;
 }
 
@@ -527,6 +523,45 @@ int itr_expm_batched_host(int n, int64_t batch, const double* h_A, double* h_out
   HIP_TRY(hipMemcpy(a.p, h_A, bytes, hipMemcpyHostToDevice));
   if (int e = itr_expm_batched(n, batch, (const double*)a.p, (double*)o.p, nullptr)) return e;
   HIP_TRY(hipMemcpy(h_out, o.p, bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int itr_solve_batched(int n, int nrhs, int64_t batch, double* M, double* R, void* stream) {
+  if (n < 1 || nrhs < 1 || batch < 0)
+    return fail(ITR_EINVAL, "bad solve shape n=%d nrhs=%d batch=%lld", n, nrhs,
+                (long long)batch);
+  if (batch == 0) return 0;
+  if (!M || !R) return fail(ITR_EINVAL, "null device pointer");
+  hipStream_t st = (hipStream_t)stream;
+  int* piv = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&piv, (size_t)batch * n * sizeof(int), st));
+  Scope sc("solve", st);
+  const hipError_t e = itr::solve_batched(n, nrhs, batch, M, R, piv, st);
+  (void)hipFreeAsync(piv, st);
+  if (e != hipSuccess) return fail(ITR_EHIP, "solve failed: %s", hipGetErrorString(e));
+  return 0;
+}
+
+int itr_gemm_batched(int m, int n, int k, int64_t batch, double alpha, const double* A,
+                     const double* B, double beta, double* C, void* stream) {
+  if (m < 1 || n < 1 || k < 1 || batch < 0)
+    return fail(ITR_EINVAL, "bad gemm shape %dx%dx%d batch=%lld", m, n, k, (long long)batch);
+  if (batch == 0) return 0;
+  if (!A || !B || !C) return fail(ITR_EINVAL, "null device pointer");
+  itr::GemmArgs g{};
+  g.m = m;
+  g.n = n;
+  g.k = k;
+  g.A = itr::Mat{(double*)A, (int64_t)m * k, k};
+  g.B = itr::Mat{(double*)B, (int64_t)k * n, n};
+  g.C = itr::Mat{C, (int64_t)m * n, n};
+  g.D = beta != 0.0 ? g.C : itr::Mat{nullptr, 0, 0};
+  g.alpha = alpha;
+  g.beta = beta;
+  g.gamma = 0.0;
+  g.idx = nullptr;
+  const hipError_t e = itr::gemm_batched(g, batch, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ITR_EHIP, "gemm failed: %s", hipGetErrorString(e));
   return 0;
 }
 

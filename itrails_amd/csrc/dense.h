@@ -1,0 +1,35 @@
+// dense.h — batched dense FP64 linear algebra for the model build (dense.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace itr {
+
+// A batch of equally shaped row-major sub-matrices: member b starts at p + slot(b)*stride.
+struct Mat {
+  double* p;
+  int64_t stride;  // elements between batch members
+  int ld;          // elements between rows
+};
+
+// C = alpha * A(m x k) @ B(k x n) + beta * D + gamma * I   (D may be null; may alias C)
+struct GemmArgs {
+  int m, n, k;
+  Mat A, B, C, D;
+  double alpha, beta, gamma;
+  const int* idx;  // batch member -> slot (null: member index)
+};
+
+hipError_t gemm_batched(const GemmArgs& g, int64_t batch, hipStream_t st);
+
+// Solve M X = R for every member (M n x n, R n x nrhs, both row-major, contiguous):
+// M is overwritten by its LU factors (partial pivoting), R by X.  `piv` is a device
+// workspace of batch * n ints.
+hipError_t solve_batched(int n, int nrhs, int64_t batch, double* M, double* R, int* piv,
+                         hipStream_t st);
+
+// out[b] = expm(A[b]) (expm.py:9-167).  Allocates its own workspace (stream-ordered).
+hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipStream_t st);
+
+}  // namespace itr

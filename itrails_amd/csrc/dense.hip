@@ -1,0 +1,617 @@
+// dense.hip — batched dense FP64 linear algebra for the iTRAILS model build on gfx950.
+//
+// The model build (get_joint_prob_mat.py, run_markov_chain_{AB,ABC}.py, vanloan.py:392-425,
+// deepest_ti.py:215-256, get_emission_prob_mat.py:22-44) spends its time in matrix
+// exponentials of CTMC rate matrices (n = 2, 4, 15, 203 and Van Loan block matrices of
+// 406 … 1015) and in one inverse per deepest-interval task.  The reference evaluates them
+// one at a time on the CPU (expm.py:9-167, numpy.linalg.solve / inv).  Here every distinct
+// matrix of a rebuild is one member of a batch, and the batch runs as:
+//
+//   * gemm_kernel      — C = alpha A B + beta D + gamma I, one 64x64 output tile per
+//                        workgroup (4 waves x 2x2 v_mfma_f64_16x16x4 tiles), K staged
+//                        through LDS 16 at a time.  All Pade products, the LU trailing
+//                        updates and the back-substitution updates run through it.
+//   * norm1_kernel     — ||A||_1 (max column sum, rows summed in order like numpy's
+//                        norm(ord=1)) selects the Pade branch per matrix (expm.py:26-140).
+//   * LU with partial pivoting, blocked by 32 columns (getrf + getrs): panel_kernel (one
+//                        workgroup per matrix, first-max |.| pivots like LAPACK idamax),
+//                        swap_kernel, trsm_lower_kernel / trsm_upper_kernel (one thread per
+//                        column, the 32x32 triangle in LDS) and gemm_kernel updates.
+//   * lincomb_kernel   — the Pade polynomial sums (b_i A^i + b_0 I), V-U and V+U.
+//
+// Branch selection and scaling follow expm.py exactly: theta = 1.5e-2, 2.5e-1, 9.5e-1, 2.1
+// select Pade 3/5/7/9; otherwise Pade 13 on A / 2^s with s = max(0, ceil(log2(norm/5.4)))
+// evaluated as ceil(log(norm/5.4)/log(2)) like expm.py:141, then s squarings
+// (np.linalg.matrix_power(r, 2**s) performs exactly s squarings).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "dense.h"
+
+namespace itr {
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------------
+// GEMM
+// ---------------------------------------------------------------------------------------
+static constexpr int GBM = 64, GBN = 64, GBK = 16;
+
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
+  __shared__ double As[GBK][GBM + 2];
+  __shared__ double Bs[GBK][GBN + 2];
+  const int tiles_n = (g.n + GBN - 1) / GBN;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int64_t slot = g.idx ? g.idx[blockIdx.y] : (int64_t)blockIdx.y;
+  const double* __restrict__ A = g.A.p + slot * g.A.stride;
+  const double* __restrict__ B = g.B.p + slot * g.B.stride;
+  const int row0 = tm * GBM, col0 = tn * GBN;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;  // this wave's 32x32 quadrant of the tile
+
+  dbl4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+  const int ar = tid >> 2, ak = (tid & 3) * 4;   // A tile: row ar, k ak..ak+3
+  const int bk = tid >> 4, bc = (tid & 15) * 4;  // B tile: k bk, cols bc..bc+3
+  for (int k0 = 0; k0 < g.k; k0 += GBK) {
+    {
+      const int gr = row0 + ar;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int gk = k0 + ak + e;
+        As[ak + e][ar] = (gr < g.m && gk < g.k) ? A[(int64_t)gr * g.A.ld + gk] : 0.0;
+      }
+      const int gk = k0 + bk;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int gc = col0 + bc + e;
+        Bs[bk][bc + e] = (gk < g.k && gc < g.n) ? B[(int64_t)gk * g.B.ld + gc] : 0.0;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < GBK; kk += 4) {
+      // v_mfma_f64_16x16x4: lane l holds A[l&15][l>>4] and B[l>>4][l&15]
+      double a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = As[kk + (l >> 4)][wr * 32 + i * 16 + (l & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = Bs[kk + (l >> 4)][wc * 32 + j * 16 + (l & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  double* __restrict__ C = g.C.p + slot * g.C.stride;
+  const double* D = g.D.p ? g.D.p + slot * g.D.stride : nullptr;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        // f64 16x16x4 result: col = l & 15, row = (l >> 4) + 4 r
+        const int row = row0 + wr * 32 + i * 16 + (l >> 4) + 4 * r;
+        const int col = col0 + wc * 32 + j * 16 + (l & 15);
+        if (row < g.m && col < g.n) {
+          double v = g.alpha * acc[i][j][r];
+          if (D) v += g.beta * D[(int64_t)row * g.D.ld + col];
+          if (row == col) v += g.gamma;
+          C[(int64_t)row * g.C.ld + col] = v;
+        }
+      }
+}
+
+hipError_t gemm_batched(const GemmArgs& g, int64_t batch, hipStream_t st) {
+  if (batch <= 0 || g.m <= 0 || g.n <= 0) return hipSuccess;
+  const int tiles = ((g.m + GBM - 1) / GBM) * ((g.n + GBN - 1) / GBN);
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535) {  // grid.y limit
+    GemmArgs h = g;
+    const int64_t nb = std::min<int64_t>(65535, batch - b0);
+    if (h.idx) {
+      h.idx = g.idx + b0;
+    } else {
+      h.A.p += b0 * g.A.stride;
+      h.B.p += b0 * g.B.stride;
+      h.C.p += b0 * g.C.stride;
+      if (h.D.p) h.D.p += b0 * g.D.stride;
+    }
+    hipLaunchKernelGGL(gemm_kernel, dim3(tiles, (unsigned)nb), dim3(256), 0, st, h);
+  }
+  return hipGetLastError();
+}
+
+static hipError_t gemm(int m, int n, int k, Mat A, Mat B, Mat C, double alpha, Mat D,
+                       double beta, double gamma, const int* idx, int64_t batch,
+                       hipStream_t st) {
+  GemmArgs g{m, n, k, A, B, C, D, alpha, beta, gamma, idx};
+  return gemm_batched(g, batch, st);
+}
+
+// ---------------------------------------------------------------------------------------
+// element-wise kernels
+// ---------------------------------------------------------------------------------------
+struct LinArgs {
+  int64_t nn;         // elements per matrix (n*n)
+  int n;              // order (for the identity term)
+  double* out;        // out[g] = cI * I + sum_t c[t] * in[t][g]
+  const double* in[4];
+  double c[4];
+  double cI;
+};
+
+__global__ void __launch_bounds__(256) lincomb_kernel(LinArgs a) {
+  const int64_t g = blockIdx.y;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < a.nn;
+       e += (int64_t)gridDim.x * 256) {
+    double v = 0.0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (a.in[t]) v += a.c[t] * a.in[t][g * a.nn + e];
+    if (e / a.n == e % a.n) v += a.cI;
+    a.out[g * a.nn + e] = v;
+  }
+}
+
+// out[g] = in[src[g]] * scale[g]
+__global__ void __launch_bounds__(256) gather_scale_kernel(int64_t nn, const double* in,
+                                                           const int* src,
+                                                           const double* scale,
+                                                           double* out) {
+  const int64_t g = blockIdx.y;
+  const double* s = in + (int64_t)src[g] * nn;
+  const double f = scale[g];
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nn;
+       e += (int64_t)gridDim.x * 256)
+    out[g * nn + e] = s[e] * f;
+}
+
+// out[dst[g]] = in[sel[g]][g]   (sel picks one of two buffers per member)
+__global__ void __launch_bounds__(256) scatter_kernel(int64_t nn, const double* in0,
+                                                      const double* in1, const int* sel,
+                                                      const int* dst, double* out) {
+  const int64_t g = blockIdx.y;
+  const double* s = (sel[g] ? in1 : in0) + g * nn;
+  double* d = out + (int64_t)dst[g] * nn;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nn;
+       e += (int64_t)gridDim.x * 256)
+    d[e] = s[e];
+}
+
+// ||A||_1 = max_j sum_i |A_ij|, rows summed in order (numpy reduces axis 0 row by row)
+__global__ void __launch_bounds__(256) norm1_kernel(int n, const double* A, double* out) {
+  __shared__ double red[256];
+  const double* M = A + (int64_t)blockIdx.x * n * n;
+  double best = 0.0;
+  for (int c = threadIdx.x; c < n; c += 256) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += fabs(M[(int64_t)i * n + c]);
+    best = fmax(best, s);
+  }
+  red[threadIdx.x] = best;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+// ---------------------------------------------------------------------------------------
+// LU with partial pivoting (blocked), then forward/back substitution on the right side
+// ---------------------------------------------------------------------------------------
+static constexpr int NB = 32;  // panel width
+
+// Factor columns [k0, k0+kb) of rows [k0, n): unblocked right-looking LU on the panel.
+__global__ void __launch_bounds__(256) panel_kernel(int n, double* Mb, int* pivb, int k0,
+                                                    int kb) {
+  __shared__ double rv[256];
+  __shared__ int ri[256];
+  double* M = Mb + (int64_t)blockIdx.x * n * n;
+  int* piv = pivb + (int64_t)blockIdx.x * n;
+  const int tid = threadIdx.x;
+  for (int j = k0; j < k0 + kb; ++j) {
+    // pivot: first row with the largest |M[i][j]|, i >= j
+    double bv = -1.0;
+    int bi = j;
+    for (int i = j + tid; i < n; i += 256) {
+      const double v = fabs(M[(int64_t)i * n + j]);
+      if (v > bv) {
+        bv = v;
+        bi = i;
+      }
+    }
+    rv[tid] = bv;
+    ri[tid] = bi;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+      if (tid < h) {
+        const double o = rv[tid + h];
+        const int oi = ri[tid + h];
+        if (o > rv[tid] || (o == rv[tid] && oi < ri[tid])) {
+          rv[tid] = o;
+          ri[tid] = oi;
+        }
+      }
+      __syncthreads();
+    }
+    const int p = ri[0];
+    if (tid == 0) piv[j] = p;
+    if (p != j && tid < kb) {
+      const int c = k0 + tid;
+      const double t = M[(int64_t)j * n + c];
+      M[(int64_t)j * n + c] = M[(int64_t)p * n + c];
+      M[(int64_t)p * n + c] = t;
+    }
+    __syncthreads();
+    const double d = M[(int64_t)j * n + j];
+    const double rd = 1.0 / d;
+    for (int i = j + 1 + tid; i < n; i += 256) {
+      double* row = M + (int64_t)i * n;
+      const double lij = row[j] * rd;
+      row[j] = lij;
+      for (int c = j + 1; c < k0 + kb; ++c) row[c] -= lij * M[(int64_t)j * n + c];
+    }
+    __syncthreads();
+  }
+}
+
+// Apply the panel's row interchanges to every column outside the panel (and to R).
+__global__ void __launch_bounds__(256) swap_kernel(int n, int nrhs, double* Mb, double* Rb,
+                                                   const int* pivb, int k0, int kb) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= n + nrhs || (c >= k0 && c < k0 + kb)) return;
+  const int* piv = pivb + (int64_t)blockIdx.y * n;
+  double* base;
+  int ld, col;
+  if (c < n) {
+    base = Mb + (int64_t)blockIdx.y * n * n;
+    ld = n;
+    col = c;
+  } else {
+    base = Rb + (int64_t)blockIdx.y * n * nrhs;
+    ld = nrhs;
+    col = c - n;
+  }
+  for (int j = k0; j < k0 + kb; ++j) {
+    const int p = piv[j];
+    if (p != j) {
+      const double t = base[(int64_t)j * ld + col];
+      base[(int64_t)j * ld + col] = base[(int64_t)p * ld + col];
+      base[(int64_t)p * ld + col] = t;
+    }
+  }
+}
+
+// rows [k0, k0+kb) of the columns right of the panel and of R: X <- L11^{-1} X
+__global__ void __launch_bounds__(256) trsm_lower_kernel(int n, int nrhs, const double* Mb,
+                                                         double* Mw, double* Rb, int k0,
+                                                         int kb) {
+  __shared__ double L[NB][NB];
+  const double* M = Mb + (int64_t)blockIdx.y * n * n;
+  for (int e = threadIdx.x; e < NB * NB; e += 256) {
+    const int r = e / NB, c = e % NB;
+    L[r][c] = (r < kb && c < kb) ? M[(int64_t)(k0 + r) * n + k0 + c] : 0.0;
+  }
+  __syncthreads();
+  const int right = n - (k0 + kb);
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= right + nrhs) return;
+  double* base;
+  int ld, col;
+  if (c < right) {
+    base = Mw + (int64_t)blockIdx.y * n * n;
+    ld = n;
+    col = k0 + kb + c;
+  } else {
+    base = Rb + (int64_t)blockIdx.y * n * nrhs;
+    ld = nrhs;
+    col = c - right;
+  }
+  double x[NB];
+#pragma unroll
+  for (int a = 0; a < NB; ++a) x[a] = a < kb ? base[(int64_t)(k0 + a) * ld + col] : 0.0;
+#pragma unroll
+  for (int a = 0; a < NB; ++a) {
+    if (a < kb) {  // rows b >= kb of L are zero-filled and their x is never stored
+#pragma unroll
+      for (int b = a + 1; b < NB; ++b) x[b] -= L[b][a] * x[a];
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < NB; ++a)
+    if (a < kb) base[(int64_t)(k0 + a) * ld + col] = x[a];
+}
+
+// rows [k0, k0+kb) of R: X <- U11^{-1} X
+__global__ void __launch_bounds__(256) trsm_upper_kernel(int n, int nrhs, const double* Mb,
+                                                         double* Rb, int k0, int kb) {
+  __shared__ double U[NB][NB];
+  const double* M = Mb + (int64_t)blockIdx.y * n * n;
+  for (int e = threadIdx.x; e < NB * NB; e += 256) {
+    const int r = e / NB, c = e % NB;
+    U[r][c] = (r < kb && c < kb) ? M[(int64_t)(k0 + r) * n + k0 + c] : 0.0;
+  }
+  __syncthreads();
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= nrhs) return;
+  double* R = Rb + (int64_t)blockIdx.y * n * nrhs;
+  double x[NB];
+#pragma unroll
+  for (int a = 0; a < NB; ++a) x[a] = a < kb ? R[(int64_t)(k0 + a) * nrhs + c] : 0.0;
+#pragma unroll
+  for (int a = NB - 1; a >= 0; --a) {
+    if (a < kb) {
+      x[a] /= U[a][a];
+#pragma unroll
+      for (int b = 0; b < a; ++b) x[b] -= U[b][a] * x[a];
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < NB; ++a)
+    if (a < kb) R[(int64_t)(k0 + a) * nrhs + c] = x[a];
+}
+
+hipError_t solve_batched(int n, int nrhs, int64_t batch, double* M, double* R, int* piv,
+                         hipStream_t st) {
+  if (batch <= 0 || n <= 0) return hipSuccess;
+  const int64_t nn = (int64_t)n * n, nr = (int64_t)n * nrhs;
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+    const int nb = (int)std::min<int64_t>(65535, batch - b0);
+    double* Mc = M + b0 * nn;
+    double* Rc = R + b0 * nr;
+    int* pc = piv + b0 * n;
+    for (int k0 = 0; k0 < n; k0 += NB) {
+      const int kb = std::min(NB, n - k0), k1 = k0 + kb;
+      hipLaunchKernelGGL(panel_kernel, dim3(nb), dim3(256), 0, st, n, Mc, pc, k0, kb);
+      hipLaunchKernelGGL(swap_kernel, dim3((n + nrhs + 255) / 256, nb), dim3(256), 0, st, n,
+                         nrhs, Mc, Rc, pc, k0, kb);
+      const int right = n - k1;
+      hipLaunchKernelGGL(trsm_lower_kernel, dim3((right + nrhs + 255) / 256, nb), dim3(256),
+                         0, st, n, nrhs, Mc, Mc, Rc, k0, kb);
+      if (right > 0) {
+        // A22 -= L21 U12 ; R2 -= L21 R1
+        Mat L21{Mc + (int64_t)k1 * n + k0, nn, n};
+        Mat U12{Mc + (int64_t)k0 * n + k1, nn, n};
+        Mat A22{Mc + (int64_t)k1 * n + k1, nn, n};
+        if (hipError_t e = gemm(right, right, kb, L21, U12, A22, -1.0, A22, 1.0, 0.0, nullptr,
+                                nb, st))
+          return e;
+        Mat R1{Rc + (int64_t)k0 * nrhs, nr, nrhs};
+        Mat R2{Rc + (int64_t)k1 * nrhs, nr, nrhs};
+        if (hipError_t e = gemm(right, nrhs, kb, L21, R1, R2, -1.0, R2, 1.0, 0.0, nullptr, nb,
+                                st))
+          return e;
+      }
+    }
+    const int last = ((n - 1) / NB) * NB;
+    for (int k0 = last; k0 >= 0; k0 -= NB) {
+      const int kb = std::min(NB, n - k0);
+      hipLaunchKernelGGL(trsm_upper_kernel, dim3((nrhs + 255) / 256, nb), dim3(256), 0, st, n,
+                         nrhs, Mc, Rc, k0, kb);
+      if (k0 > 0) {  // R[0:k0] -= U[0:k0, k0:k1] X[k0:k1]
+        Mat U01{Mc + k0, nn, n};
+        Mat X1{Rc + (int64_t)k0 * nrhs, nr, nrhs};
+        Mat R0{Rc, nr, nrhs};
+        if (hipError_t e = gemm(k0, nrhs, kb, U01, X1, R0, -1.0, R0, 1.0, 0.0, nullptr, nb,
+                                st))
+          return e;
+      }
+    }
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// expm
+// ---------------------------------------------------------------------------------------
+// Pade coefficients b_0 .. b_m (Higham 2008, Alg. 10.20; the values of expm.py:29-140)
+static const double kB3[] = {120, 60, 12, 1};
+static const double kB5[] = {30240, 15120, 3360, 420, 30, 1};
+static const double kB7[] = {17297280, 8648640, 1995840, 277200, 25200, 1512, 56, 1};
+static const double kB9[] = {17643225600.0, 8821612800.0, 2075673600.0, 302702400.0,
+                             30270240.0,    2162160.0,    110880.0,     3960.0,
+                             90.0,          1.0};
+static const double kB13[] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
+                              1187353796428800.0,  129060195264000.0,   10559470521600.0,
+                              670442572800.0,      33522128640.0,       1323241920.0,
+                              40840800.0,          960960.0,            16380.0,
+                              182.0,               1.0};
+
+static hipError_t lincomb(int n, int64_t g, double* out, std::initializer_list<const double*> in,
+                          std::initializer_list<double> c, double cI, hipStream_t st) {
+  LinArgs a{};
+  a.nn = (int64_t)n * n;
+  a.n = n;
+  a.out = out;
+  int t = 0;
+  auto ci = c.begin();
+  for (const double* p : in) {
+    a.in[t] = p;
+    a.c[t] = *ci++;
+    ++t;
+  }
+  a.cI = cI;
+  const int bx = (int)std::min<int64_t>((a.nn + 255) / 256, 64);
+  for (int64_t b0 = 0; b0 < g; b0 += 65535) {
+    LinArgs h = a;
+    const int64_t off = b0 * a.nn;
+    h.out += off;
+    for (int u = 0; u < 4; ++u)
+      if (h.in[u]) h.in[u] += off;
+    hipLaunchKernelGGL(lincomb_kernel, dim3(bx, (unsigned)std::min<int64_t>(65535, g - b0)),
+                       dim3(256), 0, st, h);
+  }
+  return hipGetLastError();
+}
+
+// one Pade branch for a chunk of G members, all of order n, already gathered + scaled into
+// W[0]; result (before squaring) in W[2]
+static hipError_t pade_chunk(int n, int64_t G, int m, double* const W[8], int* piv,
+                             hipStream_t st) {
+  const int64_t nn = (int64_t)n * n;
+  auto M = [&](int i) { return Mat{W[i], nn, n}; };
+  const Mat none{nullptr, 0, 0};
+  hipError_t e;
+#define TRY(x)                   \
+  if ((e = (x)) != hipSuccess) { \
+    return e;                    \
+  }
+  // A2 = A @ A
+  TRY(gemm(n, n, n, M(0), M(0), M(1), 1.0, none, 0.0, 0.0, nullptr, G, st));
+  if (m == 13) {
+    const double* b = kB13;
+    TRY(gemm(n, n, n, M(1), M(1), M(2), 1.0, none, 0.0, 0.0, nullptr, G, st));  // A4
+    TRY(gemm(n, n, n, M(1), M(2), M(3), 1.0, none, 0.0, 0.0, nullptr, G, st));  // A6 = A2 A4
+    // U = A (A6 (b13 A6 + b11 A4 + b9 A2) + b7 A6 + b5 A4 + b3 A2 + b1 I)
+    TRY(lincomb(n, G, W[4], {W[3], W[2], W[1]}, {b[13], b[11], b[9]}, 0.0, st));
+    TRY(lincomb(n, G, W[5], {W[3], W[2], W[1]}, {b[7], b[5], b[3]}, b[1], st));
+    TRY(gemm(n, n, n, M(3), M(4), M(6), 1.0, M(5), 1.0, 0.0, nullptr, G, st));
+    TRY(gemm(n, n, n, M(0), M(6), M(7), 1.0, none, 0.0, 0.0, nullptr, G, st));  // U -> W7
+    // V = A6 (b12 A6 + b10 A4 + b8 A2) + b6 A6 + b4 A4 + b2 A2 + b0 I
+    TRY(lincomb(n, G, W[4], {W[3], W[2], W[1]}, {b[12], b[10], b[8]}, 0.0, st));
+    TRY(lincomb(n, G, W[5], {W[3], W[2], W[1]}, {b[6], b[4], b[2]}, b[0], st));
+    TRY(gemm(n, n, n, M(3), M(4), M(6), 1.0, M(5), 1.0, 0.0, nullptr, G, st));  // V -> W6
+  } else {
+    const double* b = m == 3 ? kB3 : m == 5 ? kB5 : m == 7 ? kB7 : kB9;
+    const int np = m / 2;  // powers A2 .. A^(2 np) in W1 .. W(np)  (A2n = A2n @ A2)
+    for (int p = 2; p <= np; ++p)
+      TRY(gemm(n, n, n, M(p - 1), M(1), M(p), 1.0, none, 0.0, 0.0, nullptr, G, st));
+    // U = A (b1 I + b3 A2 + ...), V = b0 I + b2 A2 + ...
+    const double* P[4] = {W[1], np >= 2 ? W[2] : nullptr, np >= 3 ? W[3] : nullptr,
+                          np >= 4 ? W[4] : nullptr};
+    TRY(lincomb(n, G, W[5], {P[0], P[1], P[2], P[3]},
+                {b[3], np >= 2 ? b[5] : 0.0, np >= 3 ? b[7] : 0.0, np >= 4 ? b[9] : 0.0},
+                b[1], st));
+    TRY(gemm(n, n, n, M(0), M(5), M(7), 1.0, none, 0.0, 0.0, nullptr, G, st));  // U -> W7
+    TRY(lincomb(n, G, W[6], {P[0], P[1], P[2], P[3]},
+                {b[2], np >= 2 ? b[4] : 0.0, np >= 3 ? b[6] : 0.0, np >= 4 ? b[8] : 0.0},
+                b[0], st));  // V -> W6
+  }
+  // r = solve(V - U, V + U)  (expm.py:53,166)
+  TRY(lincomb(n, G, W[1], {W[6], W[7]}, {1.0, -1.0}, 0.0, st));
+  TRY(lincomb(n, G, W[2], {W[6], W[7]}, {1.0, 1.0}, 0.0, st));
+  TRY(solve_batched(n, n, G, W[1], W[2], piv, st));
+#undef TRY
+  return hipSuccess;
+}
+
+static void branch_of(double norm, int* m, int* s) {
+  *s = 0;
+  if (norm < 1.5e-2) *m = 3;
+  else if (norm < 2.5e-1) *m = 5;
+  else if (norm < 9.5e-1) *m = 7;
+  else if (norm < 2.1) *m = 9;
+  else {
+    *m = 13;
+    const double v = ceil(log(norm / 5.4) / log(2.0));
+    *s = v > 0.0 ? (int)v : 0;
+  }
+}
+
+hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipStream_t st) {
+  if (batch <= 0) return hipSuccess;
+  const int64_t nn = (int64_t)n * n;
+  hipError_t e;
+  double* d_norm = nullptr;
+  if ((e = hipMallocAsync((void**)&d_norm, batch * sizeof(double), st))) return e;
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535)
+    hipLaunchKernelGGL(norm1_kernel, dim3((unsigned)std::min<int64_t>(65535, batch - b0)),
+                       dim3(256), 0, st, n, A + b0 * nn, d_norm + b0);
+  std::vector<double> norm(batch);
+  e = hipMemcpyAsync(norm.data(), d_norm, batch * sizeof(double), hipMemcpyDeviceToHost, st);
+  if (!e) e = hipStreamSynchronize(st);
+  (void)hipFreeAsync(d_norm, st);
+  if (e) return e;
+
+  std::vector<int> m(batch), s(batch);
+  for (int64_t b = 0; b < batch; ++b) branch_of(norm[b], &m[b], &s[b]);
+
+  // chunk size: 8 work matrices per member, at most ~4 GiB of workspace per chunk
+  const int64_t per = 8 * nn * (int64_t)sizeof(double) + n * (int64_t)sizeof(int) + 64;
+  const int64_t cap = std::max<int64_t>(1, ((int64_t)4 << 30) / per);
+  for (int mm : {3, 5, 7, 9, 13}) {
+    std::vector<int> members;
+    for (int64_t b = 0; b < batch; ++b)
+      if (m[b] == mm) members.push_back((int)b);
+    for (size_t c0 = 0; c0 < members.size(); c0 += cap) {
+      const int64_t G = std::min<int64_t>(cap, members.size() - c0);
+      // host staging of the chunk's index / scale tables
+      std::vector<int> src(G), sel(G), act;
+      std::vector<double> scale(G);
+      int smax = 0;
+      for (int64_t g = 0; g < G; ++g) {
+        const int b = members[c0 + g];
+        src[g] = b;
+        scale[g] = ldexp(1.0, -s[b]);  // A /= 2**s (exact)
+        sel[g] = 0;
+        smax = std::max(smax, s[b]);
+      }
+      char* ws = nullptr;
+      const size_t bytes = (size_t)(8 * G * nn) * sizeof(double) + (size_t)G * n * sizeof(int) +
+                           (size_t)G * (3 * sizeof(int) + sizeof(double)) + 256;
+      if ((e = hipMallocAsync((void**)&ws, bytes, st))) return e;
+      double* W[8];
+      for (int i = 0; i < 8; ++i) W[i] = (double*)ws + (int64_t)i * G * nn;
+      int* piv = (int*)(W[7] + G * nn);
+      int* d_src = piv + G * n;
+      int* d_sel = d_src + G;
+      int* d_act = d_sel + G;
+      double* d_scale = (double*)(((uintptr_t)(d_act + G) + 15) & ~(uintptr_t)15);
+      e = hipMemcpyAsync(d_src, src.data(), G * sizeof(int), hipMemcpyHostToDevice, st);
+      if (!e)
+        e = hipMemcpyAsync(d_scale, scale.data(), G * sizeof(double), hipMemcpyHostToDevice, st);
+      const int bx = (int)std::min<int64_t>((nn + 255) / 256, 64);
+      for (int64_t g0 = 0; !e && g0 < G; g0 += 65535) {
+        hipLaunchKernelGGL(gather_scale_kernel,
+                           dim3(bx, (unsigned)std::min<int64_t>(65535, G - g0)), dim3(256), 0,
+                           st, nn, A, d_src + g0, d_scale + g0, W[0] + g0 * nn);
+        e = hipGetLastError();
+      }
+      if (!e) e = pade_chunk(n, G, mm, W, piv, st);
+      // s squarings, in lock-step: after level k the members with s >= k hold r^(2^k) in
+      // W[2 + (k & 1)]  (np.linalg.matrix_power(r, 2**s), expm.py:167)
+      for (int lev = 1; !e && lev <= smax; ++lev) {
+        act.clear();
+        for (int64_t g = 0; g < G; ++g)
+          if (s[members[c0 + g]] >= lev) act.push_back((int)g);
+        e = hipMemcpyAsync(d_act, act.data(), act.size() * sizeof(int), hipMemcpyHostToDevice,
+                           st);
+        if (!e) e = hipStreamSynchronize(st);  // act is reused next level
+        const Mat X{W[2 + ((lev - 1) & 1)], nn, n};
+        const Mat Y{W[2 + (lev & 1)], nn, n};
+        if (!e)
+          e = gemm(n, n, n, X, X, Y, 1.0, Mat{nullptr, 0, 0}, 0.0, 0.0, d_act,
+                   (int64_t)act.size(), st);
+      }
+      for (int64_t g = 0; g < G; ++g) sel[g] = s[members[c0 + g]] & 1;
+      if (!e) e = hipMemcpyAsync(d_sel, sel.data(), G * sizeof(int), hipMemcpyHostToDevice, st);
+      for (int64_t g0 = 0; !e && g0 < G; g0 += 65535) {
+        hipLaunchKernelGGL(scatter_kernel, dim3(bx, (unsigned)std::min<int64_t>(65535, G - g0)),
+                           dim3(256), 0, st, nn, W[2] + g0 * nn, W[3] + g0 * nn, d_sel + g0,
+                           d_src + g0, out);
+        e = hipGetLastError();
+      }
+      // host vectors must outlive the async copies
+      hipError_t e2 = hipStreamSynchronize(st);
+      (void)hipFreeAsync(ws, st);
+      if (e) return e;
+      if (e2) return e2;
+    }
+  }
+  return hipSuccess;
+}
+
+}  // namespace itr

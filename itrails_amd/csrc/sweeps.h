@@ -51,9 +51,4 @@ hipError_t launch_vit_traceback(int n, int64_t nblocks, int64_t nchunks, const i
                                 uint8_t* chunk_end, const uint8_t* bp, uint8_t* path,
                                 hipStream_t st);
 
-// batched matrix exponential (expm.hip)
-hipError_t launch_expm_batched(int n, int64_t batch, const double* A, double* out,
-                               double* work, hipStream_t st);
-size_t expm_workspace_bytes(int n, int64_t batch);
-
 }  // namespace itr

@@ -1,0 +1,90 @@
+"""Batched dense FP64 linear algebra on the GPU (itrails_amd/csrc/dense.hip) behind the
+reference's own call surface.
+
+* `expm(A)` — the reference's `expm` (expm.py:9-167): same Pade branch per 1-norm, same
+  scaling and squaring; returns a NumPy array.  `expm_batched` runs any number of matrices
+  of one order in one call (the model build batches every distinct propagator of a
+  rebuild).
+* `solve_batched`, `gemm_batched` — device LU solve / MFMA GEMM for the Van Loan and
+  deepest-interval contractions.
+
+Inputs may be NumPy arrays (copied to the current device and back) or torch.cuda float64
+tensors (used in place; results stay on the device).  No host fallback: without the
+library or a device every call raises.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import check, lib
+
+__all__ = ["expm", "expm_batched", "solve_batched", "gemm_batched"]
+
+
+def _dev(x):
+    import torch
+    if isinstance(x, torch.Tensor):
+        if not x.is_cuda or x.dtype != torch.float64:
+            raise TypeError("expected a torch.cuda float64 tensor")
+        return x.contiguous(), True
+    return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64)).cuda(), False
+
+
+def _stream():
+    import torch
+    return torch.cuda.current_stream().cuda_stream
+
+
+def expm_batched(A):
+    """expm of every A[b] (shape (B, n, n)); NumPy in -> NumPy out, CUDA tensor in -> out."""
+    import torch
+    d, on_dev = _dev(A)
+    if d.dim() != 3 or d.shape[1] != d.shape[2]:
+        raise ValueError("expected a (batch, n, n) array")
+    out = torch.empty_like(d)
+    if d.shape[0]:
+        check(lib().itr_expm_batched(d.shape[1], d.shape[0], d.data_ptr(), out.data_ptr(),
+                                     _stream()))
+    return out if on_dev else out.cpu().numpy()
+
+
+def expm(A):
+    """Matrix exponential of one square matrix (expm.py:9).  The reference divides its
+    argument in place by 2**s on the Pade-13 branch (expm.py:141-143); every reference call
+    site passes a temporary, so the argument is left untouched here."""
+    A = np.asarray(A, dtype=np.float64)
+    if A.ndim != 2 or A.shape[0] != A.shape[1]:
+        raise ValueError("expm expects a square matrix")
+    return expm_batched(A[None])[0]
+
+
+def solve_batched(M, R):
+    """X with M[b] X[b] = R[b] (LU with partial pivoting); M (B,n,n), R (B,n,k)."""
+    import torch
+    dM, on_dev = _dev(M)
+    dR, _ = _dev(R)
+    dM = dM.clone()
+    dR = dR.clone()
+    if dM.dim() != 3 or dR.dim() != 3 or dM.shape[1] != dM.shape[2] or \
+            dR.shape[:2] != dM.shape[:2]:
+        raise ValueError("expected M (batch, n, n) and R (batch, n, k)")
+    if dM.shape[0]:
+        check(lib().itr_solve_batched(dM.shape[1], dR.shape[2], dM.shape[0], dM.data_ptr(),
+                                      dR.data_ptr(), _stream()))
+    return dR if on_dev else dR.cpu().numpy()
+
+
+def gemm_batched(A, B, alpha=1.0):
+    """alpha * A[b] @ B[b] for every b."""
+    import torch
+    dA, on_dev = _dev(A)
+    dB, _ = _dev(B)
+    if dA.dim() != 3 or dB.dim() != 3 or dA.shape[0] != dB.shape[0] or dA.shape[2] != dB.shape[1]:
+        raise ValueError("shape mismatch")
+    C = torch.empty((dA.shape[0], dA.shape[1], dB.shape[2]), dtype=torch.float64,
+                    device=dA.device)
+    if dA.shape[0]:
+        check(lib().itr_gemm_batched(dA.shape[1], dB.shape[2], dA.shape[2], dA.shape[0],
+                                     float(alpha), dA.data_ptr(), dB.data_ptr(), 0.0,
+                                     C.data_ptr(), _stream()))
+    return C if on_dev else C.cpu().numpy()
