@@ -153,6 +153,19 @@ ITR_API int itr_gemm_batched(int m, int n, int k, int64_t batch, double alpha,
                              const double* d_A, const double* d_B, double beta, double* d_C,
                              void* stream);
 
+/* ---------------------------------------------------------------------------------- */
+/* model build: emission rows                                                          */
+/* ---------------------------------------------------------------------------------- */
+
+/* Emission probabilities of n_states hidden states over the 256 N-free columns.
+ * Replaces the per-state loops calc_emissions_single_JC69 / calc_emissions_double_JC69
+ * (get_emission_prob_mat.py:585-698) and the topology re-keying (871-875, 897-901).
+ * d_tables: n_states x 512 float64 per-state tables (layout in
+ * itrails_amd/model/emissions.py: kind, re-keying, the 4x4 branch transition matrices, the
+ * 4x4x4 single-coalescence and 4^4 double-coalescence integrals); d_out: n_states x 256. */
+ITR_API int itr_emission_rows(int n_states, const double* d_tables, double* d_out,
+                              void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -565,4 +565,13 @@ int itr_gemm_batched(int m, int n, int k, int64_t batch, double alpha, const dou
   return 0;
 }
 
+int itr_emission_rows(int n_states, const double* tables, double* out, void* stream) {
+  if (n_states < 0) return fail(ITR_EINVAL, "bad state count %d", n_states);
+  if (n_states == 0) return 0;
+  if (!tables || !out) return fail(ITR_EINVAL, "null device pointer");
+  const hipError_t e = itr::launch_emission(n_states, tables, out, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ITR_EHIP, "emission launch failed: %s", hipGetErrorString(e));
+  return 0;
+}
+
 }  // extern "C"

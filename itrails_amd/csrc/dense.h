@@ -32,4 +32,7 @@ hipError_t solve_batched(int n, int nrhs, int64_t batch, double* M, double* R, i
 // out[b] = expm(A[b]) (expm.py:9-167).  Allocates its own workspace (stream-ordered).
 hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipStream_t st);
 
+// emission rows (emission.hip): tables [n_states x 512] -> out [n_states x 256]
+hipError_t launch_emission(int n_states, const double* tables, double* out, hipStream_t st);
+
 }  // namespace itr

@@ -1,0 +1,256 @@
+"""Emission probabilities of the iTRAILS hidden states.
+
+Restates get_emission_prob_mat.py:701-1038 and cutpoints.py:5-45.
+
+Per hidden state (topology, i, j) the 256 N-free columns a0 b0 c0 d0 get the probability of
+the gene tree: JC69 substitution along every branch and coalescences inside interval i
+(and j).  The pieces:
+
+  * branch transition matrices P = expm(sum_k t_k Q_k) with Q = JC69(mu_k)
+    (get_emission_prob_mat.py:9-44) — 4x4 exponentials, batched on the GPU;
+  * the single-coalescence table F[a][b][c] = sum_d E[ P(a->d, s) P(d->b, s) P(d->c, t-s) ],
+    s ~ k e^{-ks} conditioned on s < t (get_emission_prob_mat.py:47-90);
+  * the double-coalescence table DD[a][b][c][d] = sum_{e,f} of the analogous two-event
+    integral for three lineages (rates 3 then 1, get_emission_prob_mat.py:93-424).
+    Both are evaluated here by expanding every JC69 factor 1/4 + (delta - 1/4) e^{-mu tau}
+    into exponentials and integrating each term exactly (`_expo_integral`), which gives
+    the reference's closed forms to rounding;
+  * the 4^6 / 4^4 contraction over ancestral nucleotides and the species re-keying of
+    topologies 2 and 3 — the HIP kernel of emission.hip (itr_emission_rows).
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+import numpy as np
+import scipy.special as sc
+
+# ---------------------------------------------------------------------------------------
+# cutpoints (cutpoints.py:5-45): quantiles of the (truncated) exponential coalescence time
+# ---------------------------------------------------------------------------------------
+
+
+def cutpoints_AB(n_int_AB: int, t_AB: float, coal_AB: float) -> np.ndarray:
+    """truncexpon.ppf(q, b=t_AB*coal_AB, scale=1/coal_AB), q = 0, 1/n, ..., 1."""
+    q = np.arange(n_int_AB + 1) / n_int_AB
+    scale = 1 / coal_AB
+    b = (t_AB - 0) / scale
+    out = np.empty(n_int_AB + 1)
+    inner = (q > 0) & (q < 1)
+    out[inner] = -sc.log1p(q[inner] * sc.expm1(-b)) * scale + 0
+    out[q == 0] = 0 * scale + 0
+    out[q == 1] = b * scale + 0
+    return out
+
+
+def cutpoints_ABC(n_int_ABC: int, coal_ABC: float) -> np.ndarray:
+    """expon.ppf(q, scale=1/coal_ABC), q = 0, 1/n, ..., 1 (last = +inf)."""
+    q = np.arange(n_int_ABC + 1) / n_int_ABC
+    scale = 1 / coal_ABC
+    out = np.empty(n_int_ABC + 1)
+    inner = (q > 0) & (q < 1)
+    out[inner] = -sc.log1p(-q[inner]) * scale + 0
+    out[q == 0] = 0.0
+    out[q == 1] = np.inf
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# coalescence integrals
+# ---------------------------------------------------------------------------------------
+_DELTA = np.eye(4) - 0.25  # JC69: P(x -> y, tau) = 1/4 + (delta_xy - 1/4) e^{-mu tau}
+
+
+def _phi(lam, t):
+    """int_0^t e^{lam s} ds."""
+    lam = np.asarray(lam, dtype=np.float64)
+    safe = np.where(lam == 0, 1.0, lam)
+    return np.where(lam == 0, t, sc.expm1(lam * t) / safe)
+
+
+def _expo_integral(terms, t):
+    """Sum of c * int_0^t e^{lam s} ds over terms [(c, lam)]."""
+    return sum(c * _phi(lam, t) for c, lam in terms)
+
+
+def single_table(t: float, mu: float, k: float) -> np.ndarray:
+    """F[a, b, c] = sum_d k/(1-e^{-kt}) int_0^t e^{-ks} P(a,d;s) P(d,b;s) P(d,c;t-s) ds
+    (p_b_c_given_a_JC69_analytical, get_emission_prob_mat.py:73-90)."""
+    al = _DELTA[:, None, None, :]   # (a, ., ., d)
+    be = _DELTA.T[None, :, None, :]  # (., b, ., d): delta(d, b)
+    ga = _DELTA.T[None, None, :, :]  # (., ., c, d): delta(d, c)
+    emt = np.exp(-mu * t)
+    # (1/4 + al x)(1/4 + be x)(1/4 + ga e^{-mu t} / x), x = e^{-mu s}, weight e^{-ks}
+    terms = [
+        (1 / 64, -k),
+        (ga * emt / 16, -k + mu),
+        ((al + be) / 16, -k - mu),
+        ((al + be) * ga * emt / 4, -k),
+        (al * be / 4, -k - 2 * mu),
+        (al * be * ga * emt, -k - mu),
+    ]
+    val = k * _expo_integral(terms, t) / (1 - np.exp(-(k * t)))
+    out = np.zeros((4, 4, 4))
+    for d in range(4):  # sum over d in order, like the reference's cumsum
+        out = out + np.broadcast_to(val, (4, 4, 4, 4))[..., d]
+    return out
+
+
+def double_table(t: float, mu: float) -> np.ndarray:
+    """DD[a, b, c, d] = sum_{e, f} of the two-coalescence integral: (a, b) -> e at s1
+    (rate 3), (e, c) -> f at s2 > s1 (rate 1), f -> d over t - s2; normalised by the
+    probability that both happen before t (JC69_analytical_integral_double,
+    get_emission_prob_mat.py:93-424, summed as in 427-441)."""
+    # indices (a, b, c, d, e, f)
+    D = _DELTA
+    al = D[:, None, None, None, :, None]          # delta(a, e)
+    be = D.T[None, :, None, None, :, None]        # delta(e, b)
+    ga = D[None, None, None, None, :, :]          # delta(e, f)
+    de = D.T[None, None, :, None, None, :]        # delta(f, c)
+    ep = D.T[None, None, None, :, None, :]        # delta(f, d)
+    # factors in s1, s2:  e^{-2 s1} e^{-s2} (rates 3 then 1: e^{-3 s1} e^{-(s2 - s1)})
+    #   (1/4 + al y1)(1/4 + be y1)          y1 = e^{-mu s1}
+    #   (1/4 + ga y2 / y1)                  y2 = e^{-mu s2}
+    #   (1/4 + de y2)
+    #   (1/4 + ep e^{-mu t} / y2)
+    emt = np.exp(-mu * t)
+    A = [(1 / 16, 0), ((al + be) / 4, 1), (al * be, 2)]        # coefficient, power of y1
+    G = [(1 / 4, 0), (ga, 1)]                                  # y2^q y1^-q
+    Dl = [(1 / 4, 0), (de, 1)]                                 # y2^u
+    Ep = [(1 / 4, 0), (ep * emt, -1)]                          # y2^-v
+    total = 0.0
+    for ca, p in A:
+        for cg, q in G:
+            for cd, u in Dl:
+                for ce, v in Ep:
+                    lam1 = -2.0 - mu * (p - q)
+                    lam2 = -1.0 - mu * (q + u + v)
+                    coef = ca * cg * cd * ce
+                    # int_0^t e^{lam2 s2} int_0^{s2} e^{lam1 s1} ds1 ds2
+                    if lam1 != 0.0:
+                        inner = (_phi(lam1 + lam2, t) - _phi(lam2, t)) / lam1
+                    elif lam2 != 0.0:
+                        inner = t * np.exp(lam2 * t) / lam2 - sc.expm1(lam2 * t) / lam2 ** 2
+                    else:
+                        inner = t * t / 2
+                    total = total + coef * inner
+    den = 1 + 0.5 / np.exp(3 * t) - 1.5 / np.exp(t)
+    val = 3 * np.broadcast_to(total, (4, 4, 4, 4, 4, 4)) / den
+    out = np.zeros((4, 4, 4, 4))
+    for e in range(4):
+        for f in range(4):
+            out = out + val[..., e, f]
+    return out
+
+
+def jc69_rate(mu: float) -> np.ndarray:
+    return np.full((4, 4), mu / 4) - np.diag([mu, mu, mu, mu])
+
+
+def branch_generator(ts, mus) -> np.ndarray:
+    """sum_k t_k Q_k (p_b_given_a, get_emission_prob_mat.py:22-44), exponentiated later."""
+    mat = np.zeros((4, 4))
+    for t, mu in zip(ts, mus):
+        mat = mat + t * jc69_rate(mu)
+    return mat
+
+
+# ---------------------------------------------------------------------------------------
+# per-state specifications (get_emission_prob_mat.py:701-1038)
+# ---------------------------------------------------------------------------------------
+ET_STRIDE = 512
+ET_KIND, ET_PERM, ET_A, ET_B, ET_C, ET_D, ET_AB, ET_F, ET_S, ET_DD = 0, 1, 16, 32, 48, 64, 80, 96, 160, 224
+
+
+def state_specs(t_A, t_B, t_AB, t_C, t_upper, t_out, coal_AB, coal_ABC, n_int_AB,
+                n_int_ABC, mu_A, mu_B, mu_C, mu_D, mu_AB, mu_ABC, cut_AB, cut_ABC):
+    """One spec per hidden state, in the reference's generation order:
+    (state, kind, perm, gens, first, second, dbl) with gens = branch generators for
+    a, b, c, d, ab (b, c and d use the reversed vectors, get_emission_prob_mat.py:612-635)."""
+    n = n_int_ABC
+    specs = []
+
+    def d_vec(jj):
+        add = t_upper + cut_ABC[n - 1] - cut_ABC[jj + 1] if jj != n - 1 else 0
+        return [t_out, add], [mu_D, mu_ABC]
+
+    def rev(v):
+        return list(reversed(v[0])), list(reversed(v[1]))
+
+    def single(a, b, c, ab, first, second, d, state, perm):
+        gens = [branch_generator(*a), branch_generator(*rev(b)), branch_generator(*rev(c)),
+                branch_generator(*rev(d)), branch_generator(*ab)]
+        specs.append((state, 0, perm, gens, first, second, None))
+
+    def double(a, b, c, tt, d, state, perm):
+        gens = [branch_generator(*a), branch_generator(*rev(b)), branch_generator(*rev(c)),
+                branch_generator(*rev(d)), None]
+        specs.append((state, 1, perm, gens, None, None, (tt, mu_ABC)))
+
+    for i in range(n):
+        for j in range(i + 1, n):
+            a = ([t_A, t_AB, cut_ABC[i]], [mu_A, mu_AB, mu_ABC])
+            b = ([t_B, t_AB, cut_ABC[i]], [mu_B, mu_AB, mu_ABC])
+            c = ([t_C, cut_ABC[i]], [mu_C, mu_ABC])
+            ab = ([cut_ABC[j] - cut_ABC[i + 1]], [mu_ABC])
+            first = (cut_ABC[i + 1] - cut_ABC[i], mu_ABC, coal_ABC)
+            second = ((cut_ABC[j + 1] - cut_ABC[j]) if j != n - 1 else t_upper, mu_ABC,
+                      coal_ABC)
+            d = d_vec(j)
+            single(a, b, c, ab, first, second, d, (1, i, j), 0)
+            single(a, c, b, ab, first, second, d, (2, i, j), 1)
+            single(b, c, a, ab, first, second, d, (3, i, j), 2)
+    for i in range(n):
+        a = ([t_A, t_AB, cut_ABC[i]], [mu_A, mu_AB, mu_ABC])
+        b = ([t_B, t_AB, cut_ABC[i]], [mu_B, mu_AB, mu_ABC])
+        c = ([t_C, cut_ABC[i]], [mu_C, mu_ABC])
+        tt = (cut_ABC[i + 1] - cut_ABC[i]) if i != n - 1 else t_upper
+        d = d_vec(i)
+        double(a, b, c, tt, d, (1, i, i), 0)
+        double(a, c, b, tt, d, (2, i, i), 1)
+        double(b, c, a, tt, d, (3, i, i), 2)
+    for i in range(n_int_AB):
+        for j in range(n):
+            a = ([t_A, cut_AB[i]], [mu_A, mu_AB])
+            b = ([t_B, cut_AB[i]], [mu_B, mu_AB])
+            c = ([t_C, cut_ABC[j]], [mu_C, mu_ABC])
+            ab = ([t_AB - cut_AB[i + 1], cut_ABC[j]], [mu_AB, mu_ABC])
+            first = (cut_AB[i + 1] - cut_AB[i], mu_AB, coal_AB)
+            second = ((cut_ABC[j + 1] - cut_ABC[j]) if j != n - 1 else t_upper, mu_ABC,
+                      coal_ABC)
+            single(a, b, c, ab, first, second, d_vec(j), (0, i, j), 0)
+    return specs
+
+
+def emission_rows(specs, la=None) -> Tuple[List[tuple], np.ndarray]:
+    """(states, b) with b[s] the 256 emission probabilities of specs[s]: the branch
+    exponentials as one GPU batch, the coalescence tables on the host, the contraction on
+    the GPU (itr_emission_rows)."""
+    if la is None:
+        from .linalg import DeviceLinalg
+        la = DeviceLinalg()
+    gens, where = [], []
+    for s, spec in enumerate(specs):
+        for g, m in enumerate(spec[3]):
+            if m is not None:
+                where.append((s, g))
+                gens.append(m)
+    P = la.expm(gens)
+    tab = np.zeros((len(specs), ET_STRIDE))
+    slot = [ET_A, ET_B, ET_C, ET_D, ET_AB]
+    for (s, g), m in zip(where, P):
+        tab[s, slot[g]:slot[g] + 16] = m.reshape(-1)
+    cache = {}
+    for s, (state, kind, perm, _, first, second, dbl) in enumerate(specs):
+        tab[s, ET_KIND] = kind
+        tab[s, ET_PERM] = perm
+        if kind == 0:
+            for key, off in ((first, ET_F), (second, ET_S)):
+                if key not in cache:
+                    cache[key] = single_table(*key).reshape(-1)
+                tab[s, off:off + 64] = cache[key]
+        else:
+            if dbl not in cache:
+                cache[dbl] = double_table(*dbl).reshape(-1)
+            tab[s, ET_DD:ET_DD + 256] = cache[dbl]
+    return [sp[0] for sp in specs], la.emission_rows(tab)

@@ -1,0 +1,125 @@
+"""Batched propagators of the model build on the GPU.
+
+Every matrix function the reference evaluates one call at a time — `expm` of interval
+propagators (get_joint_prob_mat.py:119-123, run_markov_chain_AB.py:135,
+run_markov_chain_ABC.py:347), Van Loan block exponentials (vanloan.py:392-425) and
+deepest-interval inverses (deepest_ti.py:215-256) — is requested here as a list, de-duplicated,
+assembled on the device and evaluated as one batch by the HIP kernels of dense.hip
+(itr_expm_batched / itr_solve_batched).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+Omega = Tuple[int, int]
+
+
+class DeviceLinalg:
+    """The product backend: torch.cuda for memory, dense.hip for the arithmetic."""
+
+    def __init__(self):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("the model build needs an MI355X (no host fallback)")
+        self.torch = torch
+        self.dev = torch.device("cuda", torch.cuda.current_device())
+        self.stats = {"expm": 0, "vanloan": 0, "deepest": 0}
+
+    def expm(self, mats: Sequence[np.ndarray]) -> List[np.ndarray]:
+        from ..dense import expm_batched
+        if not len(mats):
+            return []
+        by_n: Dict[int, List[int]] = {}
+        for i, m in enumerate(mats):
+            by_n.setdefault(m.shape[0], []).append(i)
+        out: List[np.ndarray] = [None] * len(mats)
+        for n, idx in by_n.items():
+            A = np.stack([np.asarray(mats[i], dtype=np.float64) for i in idx])
+            E = expm_batched(A)
+            for k, i in enumerate(idx):
+                out[i] = E[k]
+        self.stats["expm"] += len(mats)
+        return out
+
+    def _block_matrices(self, Q, masks, paths, L, scale, diag_blocks):
+        """(G, n*b, n*b) device tensor: `diag_blocks` diagonal blocks Q*scale and, between
+        consecutive classes p[i-1] -> p[i], the super-diagonal block
+        diag(mask p[i-1]) Q diag(mask p[i]) * scale (vanloan.py:415-423,
+        deepest_ti.py:236-250)."""
+        torch = self.torch
+        n = Q.shape[0]
+        b = diag_blocks
+        dQ = torch.from_numpy(Q).to(self.dev)
+        G = len(paths)
+        C = torch.zeros((G, n * b, n * b), dtype=torch.float64, device=self.dev)
+        Qs = dQ * scale if scale is not None else dQ
+        for blk in range(b):
+            C[:, blk * n:(blk + 1) * n, blk * n:(blk + 1) * n] = Qs
+        for blk in range(1, b):
+            ma = torch.from_numpy(np.stack([masks[p[blk - 1]] for p in paths]).astype(np.float64)).to(self.dev)
+            mb = torch.from_numpy(np.stack([masks[p[blk]] for p in paths]).astype(np.float64)).to(self.dev)
+            A = ma[:, :, None] * dQ[None] * mb[:, None, :]
+            if scale is not None:
+                A = A * scale
+            C[:, (blk - 1) * n:blk * n, blk * n:(blk + 1) * n] = A
+        return C
+
+    def vanloan(self, Q: np.ndarray, t: float, masks: Dict[Omega, np.ndarray],
+                paths: Sequence[Tuple[Omega, ...]]) -> List[np.ndarray]:
+        """expm(C t)[:n, -n:] for each omega path (vanloan.py:392-425)."""
+        from ..dense import expm_batched
+        n = Q.shape[0]
+        out: List[np.ndarray] = [None] * len(paths)
+        by_len: Dict[int, List[int]] = {}
+        for i, p in enumerate(paths):
+            by_len.setdefault(len(p), []).append(i)
+        for L, idx in sorted(by_len.items()):
+            C = self._block_matrices(Q, masks, [paths[i] for i in idx], L, float(t), L)
+            E = expm_batched(C)[:, :n, -n:].cpu().numpy()
+            for k, i in enumerate(idx):
+                out[i] = E[k]
+        self.stats["vanloan"] += len(paths)
+        return out
+
+    def deepest(self, Q: np.ndarray, masks: Dict[Omega, np.ndarray],
+                paths: Sequence[Tuple[Omega, ...]]) -> List[np.ndarray]:
+        """(-C^-1)[:n, -n:] @ (diag(m p[-2]) Q diag(m p[-1])) for each omega path
+        (deepest_ti.py:215-256); the last n columns of C^-1 come from one batched solve
+        against the last n columns of the identity."""
+        from ..dense import solve_batched
+        torch = self.torch
+        n = Q.shape[0]
+        out: List[np.ndarray] = [None] * len(paths)
+        by_len: Dict[int, List[int]] = {}
+        for i, p in enumerate(paths):
+            by_len.setdefault(len(p), []).append(i)
+        dQ = torch.from_numpy(Q).to(self.dev)
+        for L, idx in sorted(by_len.items()):
+            steps = L - 1
+            sub = [paths[i] for i in idx]
+            C = self._block_matrices(Q, masks, sub, steps, None, steps)
+            G = len(sub)
+            R = torch.zeros((G, n * steps, n), dtype=torch.float64, device=self.dev)
+            R[:, (steps - 1) * n:, :] = torch.eye(n, dtype=torch.float64, device=self.dev)
+            X = solve_batched(C, R)[:, :n, :]
+            ma = torch.from_numpy(np.stack([masks[p[-2]] for p in sub]).astype(np.float64)).to(self.dev)
+            mb = torch.from_numpy(np.stack([masks[p[-1]] for p in sub]).astype(np.float64)).to(self.dev)
+            A = (ma[:, :, None] * dQ[None] * mb[:, None, :]).contiguous()
+            from ..dense import gemm_batched
+            D = gemm_batched(X.contiguous(), A, alpha=-1.0).cpu().numpy()
+            for k, i in enumerate(idx):
+                out[i] = D[k]
+        self.stats["deepest"] += len(paths)
+        return out
+
+    def emission_rows(self, tables: np.ndarray) -> np.ndarray:
+        """Emission rows of every state from its packed tables (emission.hip)."""
+        from .._lib import check, lib
+        torch = self.torch
+        dt = torch.from_numpy(np.ascontiguousarray(tables, dtype=np.float64)).to(self.dev)
+        out = torch.empty((tables.shape[0], 256), dtype=torch.float64, device=self.dev)
+        check(lib().itr_emission_rows(tables.shape[0], dt.data_ptr(), out.data_ptr(),
+                                      torch.cuda.current_stream().cuda_stream))
+        return out.cpu().numpy()
