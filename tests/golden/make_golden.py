@@ -37,7 +37,7 @@ def _import_reference():
     sys.path.insert(0, REF_SRC)
     import itrails.ncpu as ncpu
 
-    ncpu.update_n_cpu(1)
+    ncpu.update_n_cpu(int(os.environ.get("GOLDEN_NCPU", "1")))
     return ncpu
 
 
@@ -63,6 +63,7 @@ MODELS = {
     "alt_3_2": ("alt", 3, 2),
     "kat_4_4": ("kat", 4, 4),
     "kat_5_5": ("kat", 5, 5),
+    "kat_7_7": ("kat", 7, 7),
 }
 
 
