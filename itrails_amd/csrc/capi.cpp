@@ -148,8 +148,9 @@ int check_plan(itr_plan_t p) {
 }
 
 int reserve(itr_plan_t p, int n, bool vit, bool post) {
-  const int xr = itr::sweep_row_stride(n);
-  if (xr < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", n);
+  const int xr = itr::sweep_row_stride(n, itr::MODE_VIT);
+  const int xa = itr::sweep_row_stride(n, itr::MODE_BWD);
+  if (xr < 0 || xa < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", n);
   if (vit) {
     const size_t need = (size_t)p->total * xr;
     if (need > p->bp_cap) {
@@ -165,7 +166,7 @@ int reserve(itr_plan_t p, int n, bool vit, bool post) {
     }
   }
   if (post) {
-    const size_t need = (size_t)p->total * xr;
+    const size_t need = (size_t)p->total * xa;
     if (need > p->alpha_cap) {
       dev_free(p->d_alpha);
       if (int e = dev_alloc(&p->d_alpha, need)) return e;

@@ -254,8 +254,10 @@ struct Occ {
   static constexpr int narrow = RJN * IQ <= 27 ? 3 : RJN * IQ <= 64 ? 2 : 1;
   static constexpr int base = WV == 4 ? narrow : wide;
   static constexpr int wgs = (MODE == MODE_BWD && base > 1) ? base - 1 : base;
-  // launch_bounds' second argument is waves per SIMD: WGs per CU x waves per WG / 4
-  static constexpr int value = (wgs * WV + 3) / 4;
+  // launch_bounds' second argument is waves per SIMD.  A workgroup's waves are spread
+  // round-robin over the 4 SIMDs starting at SIMD 0, so every co-resident workgroup puts
+  // ceil(W/4) waves on SIMD 0: budget for that, not for the average.
+  static constexpr int value = wgs * ((WV + 3) / 4);
 };
 
 template <int WV, int RJN, int IQ, int MODE>
@@ -772,24 +774,28 @@ struct Cfg {
 // on each SIMD (a lone wave issues FP64 at about half the SIMD's rate) and the slots pad N
 // by at most 7
 static constexpr Cfg kCfgs[] = {
-    // four waves (one per SIMD), several targets per lane: best throughput per CU (several
-    // workgroups co-resident); chosen automatically
+    // four waves (one per SIMD), several targets per lane: fewest instructions per column,
+    // several workgroups per CU
     {4, 1, 4}, {4, 2, 8}, {4, 3, 9}, {4, 3, 12}, {4, 4, 16}, {4, 5, 17}, {4, 6, 24},
-    // one target per lane, W = ceil(N/8) waves: ~25% lower step latency for a single long
-    // block but one workgroup per CU (experiments: ITR_SWEEP_CFG=7..13)
+    // one target per lane, W = ceil(N/8) waves (2-3 per SIMD): lower step latency, and with
+    // the SIMD-0 register budget two workgroups still fit per CU
     {4, 1, 4}, {8, 1, 8}, {9, 1, 9}, {12, 1, 12}, {16, 1, 16}, {9, 2, 17}, {8, 3, 24}};
-static constexpr int kAutoCfgs = 7;  // entries pick_cfg chooses from
+static constexpr int kNarrow = 7;  // entries 0..6
 
-static int pick_cfg(int n) {
+static bool fits(int c, int n) { return 8 * kCfgs[c].w * kCfgs[c].rj >= n && Q * kCfgs[c].iq >= n; }
+
+// Measured on the (5,5) model, 10 Mbp: the forward / backward sweeps run
+// fastest on the four-wave kernels; Viterbi (5 VALU instructions per pair) on the
+// one-target-per-lane kernel for N <= 72.
+static int pick_cfg(int n, int mode) {
   const char* force = getenv("ITR_SWEEP_CFG");  // experiments: force a configuration
   if (force) {
     const int c = atoi(force);
-    if (c >= 0 && c < (int)(sizeof kCfgs / sizeof kCfgs[0]) &&
-        8 * kCfgs[c].w * kCfgs[c].rj >= n && Q * kCfgs[c].iq >= n)
-      return c;
+    if (c >= 0 && c < (int)(sizeof kCfgs / sizeof kCfgs[0]) && fits(c, n)) return c;
   }
-  for (int c = 0; c < kAutoCfgs; ++c)
-    if (8 * kCfgs[c].w * kCfgs[c].rj >= n && Q * kCfgs[c].iq >= n) return c;
+  if (mode == MODE_VIT && n > 64 && n <= 72) return 9;
+  for (int c = 0; c < kNarrow; ++c)
+    if (fits(c, n)) return c;
   return -1;
 }
 
@@ -859,7 +865,7 @@ static hipError_t dispatch_mode(int mode, int cfg, bool launch, const SweepArgs*
 
 SweepGeometry sweep_geometry(int n, int mode) {
   SweepGeometry g{};
-  g.iq = pick_cfg(n);  // configuration index (negative: unsupported)
+  g.iq = pick_cfg(n, mode);  // configuration index (negative: unsupported)
   g.xp = 0;
   if (g.iq < 0) return g;
   g.block = 64 * kCfgs[g.iq].w;
@@ -878,8 +884,8 @@ hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepA
   return dispatch_mode(mode, g.iq, true, &a, grid, g.lds, st, &occ);
 }
 
-int sweep_row_stride(int n) {  // padded target states: row stride of bp / alpha rows
-  const int c = pick_cfg(n);
+int sweep_row_stride(int n, int mode) {  // padded target states: row stride of bp / alpha
+  const int c = pick_cfg(n, mode);
   return c < 0 ? -1 : 8 * kCfgs[c].w * kCfgs[c].rj;
 }
 
@@ -891,7 +897,7 @@ hipError_t launch_vit_traceback(int n, int64_t nblocks, int64_t nchunks, const i
   if (nblocks > 0) {
     const int tb = 256;
     hipLaunchKernelGGL(vit_chain_kernel, dim3((unsigned)((nblocks + tb - 1) / tb)), dim3(tb),
-                       0, st, sweep_row_stride(n), nblocks, off, chunk_base, chunk_map, last_state,
+                       0, st, sweep_row_stride(n, MODE_VIT), nblocks, off, chunk_base, chunk_map, last_state,
                        chunk_end);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -899,7 +905,7 @@ hipError_t launch_vit_traceback(int n, int64_t nblocks, int64_t nchunks, const i
   if (nchunks > 0) {
     const int tb = 256;
     hipLaunchKernelGGL(vit_fill_kernel, dim3((unsigned)((nchunks + tb - 1) / tb)), dim3(tb), 0,
-                       st, sweep_row_stride(n), nchunks, off, chunk_base, chunk_blk, chunk_end, bp,
+                       st, sweep_row_stride(n, MODE_VIT), nchunks, off, chunk_base, chunk_blk, chunk_end, bp,
                        path);
     return hipGetLastError();
   }

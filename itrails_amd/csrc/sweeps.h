@@ -42,7 +42,9 @@ struct SweepGeometry {
 };
 
 SweepGeometry sweep_geometry(int n, int mode);
-int sweep_row_stride(int n);  // row stride (padded states) of back-pointer / forward rows
+// row stride (padded states) of the back-pointer rows (MODE_VIT) / forward rows (FWD_STORE,
+// BWD: both use the same configuration)
+int sweep_row_stride(int n, int mode);
 hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepArgs& a,
                         hipStream_t st);
 hipError_t launch_vit_traceback(int n, int64_t nblocks, int64_t nchunks, const int64_t* off,

@@ -25,7 +25,8 @@ def test_oracle_vs_reference(name):
 
 
 def test_fixture_paths_switch_states():
-    # a backtracking bug is invisible on paths that never leave one state
-    for name in sweep_fixtures():
+    # a backtracking bug is invisible on paths that never leave one state; the
+    # reference's own models barely switch, so the synthetic fixtures carry this check
+    for name in [f for f in sweep_fixtures() if f.startswith("sweep_syn")]:
         g = golden(name)
         assert (np.diff(g["path"]) != 0).sum() > 5, name
