@@ -36,12 +36,14 @@ extern "C" {
 #define ITR_EINVAL 1   /* bad argument (shape, range, null pointer)           */
 #define ITR_EHIP 2     /* HIP runtime error (allocation, launch, copy)         */
 #define ITR_ESTATE 3   /* object used in the wrong state                       */
+#define ITR_EDATA 4    /* input data outside the alphabet (the reference's ValueError) */
 
 #define ITR_NOBS 625   /* observed alphabet size, read_data.py:6-24            */
 #define ITR_MAX_STATES 192
 
 typedef struct itr_model* itr_model_t; /* HMM tables resident on one device          */
 typedef struct itr_plan* itr_plan_t;   /* block layout of one alignment + workspace   */
+typedef struct itr_maf* itr_maf_t;     /* a parsed MAF file (host memory)              */
 
 /* ---------------------------------------------------------------------------------- */
 /* library                                                                             */
@@ -165,6 +167,27 @@ ITR_API int itr_gemm_batched(int m, int n, int k, int64_t batch, double alpha,
  * 4x4x4 single-coalescence and 4^4 double-coalescence integrals); d_out: n_states x 256. */
 ITR_API int itr_emission_rows(int n_states, const double* d_tables, double* d_out,
                               void* stream);
+
+/* ---------------------------------------------------------------------------------- */
+/* MAF ingest (host)                                                                   */
+/* ---------------------------------------------------------------------------------- */
+
+/* Parse a MAF file into the concatenated observation layout of the plans.
+ * Replaces maf_parser (read_data.py:94-117: blocks holding all 4 species of `species`,
+ * '-' -> 'N', upper-cased, column symbol = index in the 625-letter alphabet; a letter
+ * outside A/C/T/G/N fails with ITR_EDATA like the reference's list.index ValueError) and,
+ * when `ref` is not NULL, parse_coordinates (read_data.py:150-220: per-column reference
+ * positions, -9 for gaps / blocks without the reference).  The file is memory-mapped and
+ * scanned once. */
+ITR_API int itr_maf_open(const char* path, const char* const* species /* [4] */,
+                         const char* ref, itr_maf_t* out);
+ITR_API int itr_maf_sizes(itr_maf_t maf, int64_t* n_blocks, int64_t* n_columns,
+                          int64_t* n_coord_blocks, int64_t* n_coords);
+/* copy out: obs [n_columns], block_off [n_blocks+1], coords [n_coords],
+ * coord_off [n_coord_blocks+1]; any pointer may be NULL */
+ITR_API int itr_maf_copy(itr_maf_t maf, uint16_t* h_obs, int64_t* h_block_off,
+                         int64_t* h_coords, int64_t* h_coord_off);
+ITR_API int itr_maf_close(itr_maf_t maf);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ITR_LIB") or os.path.join(HERE, "libitrails_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "itrails_hip.h")
 
-ITR_OK, ITR_EINVAL, ITR_EHIP, ITR_ESTATE = 0, 1, 2, 3
+ITR_OK, ITR_EINVAL, ITR_EHIP, ITR_ESTATE, ITR_EDATA = 0, 1, 2, 3, 4
 NOBS = 625
 MAX_STATES = 192
 
@@ -48,6 +48,12 @@ _SIGNATURES = {
     "itr_solve_batched": ([_I, _I, _I64, _P, _P, _P], _I),
     "itr_gemm_batched": ([_I, _I, _I, _I64, _D, _P, _P, _D, _P, _P], _I),
     "itr_emission_rows": ([_I, _P, _P, _P], _I),
+    "itr_maf_open": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_char_p,
+                      ctypes.POINTER(_P)], _I),
+    "itr_maf_sizes": ([_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I64),
+                       ctypes.POINTER(_I64)], _I),
+    "itr_maf_copy": ([_P, _P, _P, _P, _P], _I),
+    "itr_maf_close": ([_P], _I),
 }
 
 

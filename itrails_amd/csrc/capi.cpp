@@ -12,6 +12,7 @@
 
 #include "../../include/itrails_hip.h"
 #include "dense.h"
+#include "maf.h"
 #include "sweeps.h"
 
 namespace {
@@ -572,6 +573,54 @@ int itr_emission_rows(int n_states, const double* tables, double* out, void* str
   if (!tables || !out) return fail(ITR_EINVAL, "null device pointer");
   const hipError_t e = itr::launch_emission(n_states, tables, out, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ITR_EHIP, "emission launch failed: %s", hipGetErrorString(e));
+  return 0;
+}
+
+struct itr_maf {
+  itr::MafResult r;
+};
+
+int itr_maf_open(const char* path, const char* const* species, const char* ref,
+                 itr_maf_t* out) {
+  if (!out) return fail(ITR_EINVAL, "null output pointer");
+  *out = nullptr;
+  if (!path || !species) return fail(ITR_EINVAL, "null path or species list");
+  for (int k = 0; k < 4; ++k)
+    if (!species[k]) return fail(ITR_EINVAL, "species list needs 4 names");
+  auto* h = new itr_maf();
+  std::string err;
+  const int rc = itr::maf_read(path, species, ref, &h->r, &err);
+  if (rc) {
+    delete h;
+    return fail(rc == 2 ? ITR_EDATA : ITR_EINVAL, "%s", err.c_str());
+  }
+  *out = h;
+  return 0;
+}
+
+int itr_maf_sizes(itr_maf_t h, int64_t* n_blocks, int64_t* n_columns, int64_t* n_coord_blocks,
+                  int64_t* n_coords) {
+  if (!h) return fail(ITR_EINVAL, "null MAF handle");
+  if (n_blocks) *n_blocks = (int64_t)h->r.off.size() - 1;
+  if (n_columns) *n_columns = (int64_t)h->r.obs.size();
+  if (n_coord_blocks) *n_coord_blocks = (int64_t)h->r.coord_off.size() - 1;
+  if (n_coords) *n_coords = (int64_t)h->r.coords.size();
+  return 0;
+}
+
+int itr_maf_copy(itr_maf_t h, uint16_t* obs, int64_t* block_off, int64_t* coords,
+                 int64_t* coord_off) {
+  if (!h) return fail(ITR_EINVAL, "null MAF handle");
+  const auto& r = h->r;
+  if (obs && !r.obs.empty()) memcpy(obs, r.obs.data(), r.obs.size() * sizeof(uint16_t));
+  if (block_off) memcpy(block_off, r.off.data(), r.off.size() * sizeof(int64_t));
+  if (coords && !r.coords.empty()) memcpy(coords, r.coords.data(), r.coords.size() * sizeof(int64_t));
+  if (coord_off) memcpy(coord_off, r.coord_off.data(), r.coord_off.size() * sizeof(int64_t));
+  return 0;
+}
+
+int itr_maf_close(itr_maf_t h) {
+  delete h;
   return 0;
 }
 
