@@ -189,6 +189,24 @@ ITR_API int itr_maf_copy(itr_maf_t maf, uint16_t* h_obs, int64_t* h_block_off,
                          int64_t* h_coords, int64_t* h_coord_off);
 ITR_API int itr_maf_close(itr_maf_t maf);
 
+/* ---------------------------------------------------------------------------------- */
+/* result files (host)                                                                 */
+/* ---------------------------------------------------------------------------------- */
+
+/* Viterbi segments CSV, byte-identical to workflow_viterbi.py:690-743 (csv excel dialect):
+ * one row per run of equal states per block; with h_coords (per-column reference
+ * positions, -9 = gap; NULL = block-relative positions) the reference's gap handling. */
+ITR_API int itr_write_viterbi_csv(const char* path, const uint8_t* h_states,
+                                  const int64_t* h_block_off, int64_t n_blocks,
+                                  const int64_t* h_coords);
+/* Posterior CSV, byte-identical to workflow_posterior.py:697-716: one row per column,
+ * probabilities printed like Python repr(float); formatted by `threads` threads. */
+ITR_API int itr_write_posterior_csv(const char* path, const double* h_post, int n_states,
+                                    const int64_t* h_block_off, int64_t n_blocks,
+                                    const int64_t* h_coords, int threads);
+/* Python repr(float) of x into out (cap >= 33 bytes suffices). */
+ITR_API int itr_format_float(double x, char* out, int cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,6 +54,9 @@ _SIGNATURES = {
                        ctypes.POINTER(_I64)], _I),
     "itr_maf_copy": ([_P, _P, _P, _P, _P], _I),
     "itr_maf_close": ([_P], _I),
+    "itr_write_viterbi_csv": ([ctypes.c_char_p, _P, _P, _I64, _P], _I),
+    "itr_write_posterior_csv": ([ctypes.c_char_p, _P, _I, _P, _I64, _P, _I], _I),
+    "itr_format_float": ([_D, ctypes.c_char_p, _I], _I),
 }
 
 

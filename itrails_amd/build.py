@@ -8,7 +8,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["hmm_sweeps.hip", "dense.hip", "emission.hip", "maf.cpp", "capi.cpp"]
+SOURCES = ["hmm_sweeps.hip", "dense.hip", "emission.hip", "maf.cpp", "writers.cpp", "capi.cpp"]
 OUT = os.path.join(HERE, "libitrails_hip.so")
 ARCH = os.environ.get("ITR_OFFLOAD_ARCH", "gfx950")
 

@@ -13,6 +13,7 @@
 #include "../../include/itrails_hip.h"
 #include "dense.h"
 #include "maf.h"
+#include "writers.h"
 #include "sweeps.h"
 
 namespace {
@@ -621,6 +622,36 @@ int itr_maf_copy(itr_maf_t h, uint16_t* obs, int64_t* block_off, int64_t* coords
 
 int itr_maf_close(itr_maf_t h) {
   delete h;
+  return 0;
+}
+
+int itr_format_float(double x, char* out, int cap) {
+  char b[40];
+  const int n = itr::format_pyfloat(x, b);
+  if (!out || cap < n + 1) return fail(ITR_EINVAL, "buffer too small");
+  memcpy(out, b, n);
+  out[n] = 0;
+  return 0;
+}
+
+int itr_write_viterbi_csv(const char* path, const uint8_t* states, const int64_t* block_off,
+                          int64_t n_blocks, const int64_t* coords) {
+  if (!path || (n_blocks > 0 && (!states || !block_off)) || n_blocks < 0)
+    return fail(ITR_EINVAL, "bad arguments");
+  std::string err;
+  if (itr::write_viterbi_csv(path, states, block_off, n_blocks, coords, &err))
+    return fail(ITR_EINVAL, "%s", err.c_str());
+  return 0;
+}
+
+int itr_write_posterior_csv(const char* path, const double* post, int n_states,
+                            const int64_t* block_off, int64_t n_blocks, const int64_t* coords,
+                            int threads) {
+  if (!path || n_states < 0 || n_blocks < 0 || (n_blocks > 0 && (!post || !block_off)))
+    return fail(ITR_EINVAL, "bad arguments");
+  std::string err;
+  if (itr::write_posterior_csv(path, post, n_states, block_off, n_blocks, coords, threads, &err))
+    return fail(ITR_EINVAL, "%s", err.c_str());
   return 0;
 }
 
