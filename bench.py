@@ -35,8 +35,9 @@ def load_model(n_int: int):
         g = np.load(f)
         return g["a"], g["b"], g["pi"], f"itrails ({n_int},{n_int}) KAT model"
     # same state count, random HMM (only until the reference model fixture exists)
-    g = np.load(os.path.join(ROOT, "tests", "golden", "sweep_syn70.npz"))
-    return g["a"], g["b"], g["pi"], "random N=70 HMM (sweep_syn70 fixture)"
+    n = {5: 70, 7: 133}.get(n_int, 70)
+    g = np.load(os.path.join(ROOT, "tests", "golden", f"sweep_syn{n}.npz"))
+    return g["a"], g["b"], g["pi"], f"random N={n} HMM (sweep_syn{n} fixture)"
 
 
 def main():
@@ -45,6 +46,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n-int", type=int, default=5)
+    ap.add_argument("--mode", choices=["fv", "posterior"], default="fv",
+                    help="fv: forward + Viterbi (BASELINE config 2, the default); posterior: "
+                         "posterior decoding (config 3)")
     ap.add_argument("--mbp", type=float, default=10.0, help="columns per GPU (Mbp)")
     ap.add_argument("--mean-block", type=float, default=2000.0)
     ap.add_argument("--cpu-sample", type=int, default=10_000_000,
@@ -81,10 +85,12 @@ def main():
 
     model = hmm.Model(a, b, pi)
     plan = hmm.Plan(off)
-    plan.reserve(n, posterior=False)
+    post_mode = args.mode == "posterior"
+    plan.reserve(n, posterior=post_mode)
     d_obs = torch.from_numpy(obs.astype(np.int16)).to(dev)
     d_ll = torch.empty(plan.nblocks, dtype=torch.float64, device=dev)
     d_path = torch.empty(plan.total, dtype=torch.uint8, device=dev)
+    d_post = torch.empty((plan.total, n), dtype=torch.float64, device=dev) if post_mode else None
     nblk_global = plan.nblocks
     if world > 1:
         counts = torch.tensor([plan.nblocks], device=dev)
@@ -98,6 +104,13 @@ def main():
     fwd_ms, vit_ms, tb_ms = [], [], []
 
     def step(timing=False):
+        if post_mode:
+            hmm.posterior_device(model, plan, d_obs, out=d_post)
+            if timing:
+                fwd_ms.append(hmm.last_kernel_ms("posterior_fwd"))
+                vit_ms.append(hmm.last_kernel_ms("posterior_bwd"))
+                tb_ms.append(0.0)
+            return
         hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
         if timing:
             fwd_ms.append(hmm.last_kernel_ms("forward"))
@@ -147,18 +160,21 @@ def main():
     result = None
     if rank == 0:
         vit_avg = float(np.mean(vit_ms))
-        ops_per_col = 2.0 * n * n  # Viterbi: one add + one max per (i, j) pair
+        # Viterbi: one add + one max per (i, j) pair; backward: one FMA
+        ops_per_col = 2.0 * n * n
         achieved = ops_per_col * cols / (vit_avg * 1e-3) / 1e12
-        traffic, traffic_note = pmc_traffic(n)
+        traffic, traffic_note = pmc_traffic(n, 2 if post_mode else 3)
         cpu = None
         if args.cpu_sample > 0:
-            cpu = cpu_baseline(a, b, pi, obs, off, args.cpu_sample, args.cpu_seconds)
+            cpu = cpu_baseline(a, b, pi, obs, off, args.cpu_sample, args.cpu_seconds,
+                               post_mode)
         check = None
-        if args.check:
+        if args.check and not post_mode:
             check = verify(a, b, pi, obs, off, ll_host if world == 1 else d_ll.cpu().numpy(),
                            d_path.cpu().numpy())
         result = {
-            "metric": "alignment columns/s (forward+Viterbi), 3sp+outgroup HMM",
+            "metric": ("alignment columns/s (posterior decoding), 3sp+outgroup HMM" if post_mode
+                       else "alignment columns/s (forward+Viterbi), 3sp+outgroup HMM"),
             "value": round(value, 1),
             "unit": "columns/s",
             "n_gpus": world,
@@ -171,13 +187,15 @@ def main():
             "dtype": "f64",
             "data": "synthetic: columns sampled from the reference's (5,5) KAT model, "
                     "geometric blocks mean 2 kbp, 1% gaps + 0.5% N",
-            "config": {"workload": f"{args.mbp:g} Mbp/GPU, {n_int_label(args.n_int)}, "
-                                   "forward loglik + Viterbi traceback",
+            "config": {"workload": f"{args.mbp:g} Mbp/GPU, {n_int_label(args.n_int)}, " +
+                                   ("posterior decoding" if post_mode else
+                                    "forward loglik + Viterbi traceback"),
                        "model": model_name, "hidden_states": n,
                        "columns_per_gpu": cols, "blocks_per_gpu": int(plan.nblocks),
                        "longest_block": int(np.diff(off).max()),
                        "parallelism": f"block-sharded x{world}"},
-            "roofline": {"kernel": "sweep_kernel<VIT> (Viterbi max-plus)",
+            "roofline": {"kernel": ("sweep_kernel<BWD> (backward + posterior)" if post_mode
+                                    else "sweep_kernel<VIT> (Viterbi max-plus)"),
                          "bound": "mfma", "pipe": "FP64 VALU (add/max; FP64 vector rate = "
                                                   "FP64 matrix rate on MI355X)",
                          "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
@@ -204,7 +222,7 @@ def n_int_label(k):
     return f"{k}+{k} intervals"
 
 
-def pmc_traffic(n):
+def pmc_traffic(n, mode=3):
     """HBM bytes per Viterbi launch from the committed rocprofv3 PMC summary of this same
     command (scripts/gpu_profile.sh -> scripts/summarize_profile.py -> profiles/*_summary.json:
     FETCH_SIZE + WRITE_SIZE, separate passes).  None when no summary for this model size."""
@@ -213,7 +231,7 @@ def pmc_traffic(n):
     for f in reversed(files):
         d = json.load(open(f))
         for name, v in d.items():
-            if name.startswith("void itr::sweep_kernel<") and name.endswith(", 3>(itr::SweepArgs)") \
+            if name.startswith("void itr::sweep_kernel<") and name.endswith(f", {mode}>(itr::SweepArgs)") \
                     and v.get("n_states", 70) == n and "hbm_bytes_raw" in v:
                 return round(v["hbm_bytes_raw"]), (
                     f"{os.path.basename(f)}: FETCH_SIZE+WRITE_SIZE per launch (raw; "
@@ -221,7 +239,7 @@ def pmc_traffic(n):
     return None, "no PMC summary under profiles/"
 
 
-def cpu_baseline(a, b, pi, obs, off, sample_cols, min_seconds=10.0):
+def cpu_baseline(a, b, pi, obs, off, sample_cols, min_seconds=10.0, posterior=False):
     """The repo's C restatement of the reference sweeps (oracle/, OpenMP over blocks),
     forward + Viterbi on a bounded prefix of this rank's blocks, repeated until min_seconds
     have passed."""
@@ -239,8 +257,11 @@ def cpu_baseline(a, b, pi, obs, off, sample_cols, min_seconds=10.0):
     t0 = time.perf_counter()
     reps = 0
     while True:
-        O.forward_loglik(t, ob, o2)
-        O.viterbi(t, ob, o2)
+        if posterior:
+            O.posterior(t, ob, o2)
+        else:
+            O.forward_loglik(t, ob, o2)
+            O.viterbi(t, ob, o2)
         reps += 1
         dt = time.perf_counter() - t0
         if dt >= min_seconds or reps >= 20:
@@ -248,7 +269,8 @@ def cpu_baseline(a, b, pi, obs, off, sample_cols, min_seconds=10.0):
     return {"value": round(float(o2[-1]) * reps / dt, 1), "unit": "columns/s", "cores": cores,
             "kind": "port",
             "sample": f"first {nb} blocks ({int(o2[-1])} columns) of the same workload, "
-                      f"forward + Viterbi, {reps} pass(es), {dt:.2f} s"}
+                      f"{'posterior' if posterior else 'forward + Viterbi'}, {reps} pass(es), "
+                      f"{dt:.2f} s"}
 
 
 def verify(a, b, pi, obs, off, ll, path):

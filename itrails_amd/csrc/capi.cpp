@@ -118,6 +118,7 @@ struct itr_plan {
   int64_t *d_off = nullptr, *d_chunk_base = nullptr;
   int32_t *d_order = nullptr, *d_chunk_blk = nullptr;
   int* d_queue = nullptr;
+  double* d_sink = nullptr;  // write target of padded states (64 doubles)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
   // workspace (grown on demand)
   uint8_t* d_bp = nullptr;
@@ -185,6 +186,7 @@ itr::SweepArgs base_args(itr_model_t m, itr_plan_t p, const uint16_t* obs) {
   a.off = p->d_off;
   a.order = p->d_order;
   a.queue = p->d_queue;
+  a.sink = p->d_sink;
   a.obs = obs;
   a.chunk_base = p->d_chunk_base;
   a.prio_len = p->prio_len;
@@ -325,6 +327,7 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   if (!e) e = dev_alloc(&p->d_chunk_base, nblocks);
   if (!e) e = dev_alloc(&p->d_chunk_blk, nc);
   if (!e) e = dev_alloc(&p->d_queue, 4);
+  if (!e) e = dev_alloc(&p->d_sink, 64);
   if (!e) e = dev_alloc(&p->d_chunk_end, nc);
   if (!e) e = dev_alloc(&p->d_last, nblocks);
   auto up = [&](void* d, const void* h, size_t bytes) {
@@ -351,6 +354,7 @@ int itr_plan_destroy(itr_plan_t p) {
   dev_free(p->d_chunk_base);
   dev_free(p->d_chunk_blk);
   dev_free(p->d_queue);
+  dev_free(p->d_sink);
   dev_free(p->d_bp);
   dev_free(p->d_chunk_map);
   dev_free(p->d_chunk_end);

@@ -496,76 +496,84 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
         // ------------- backward + posterior (optimizer.py:191-238)
         //   beta_{T-1} = 1;  beta_{t-1} = (beta_t * e_t) @ a  (vector @ a: the reference's form)
         //   post_t = alpha_t * beta_t / sum_j(alpha_t * beta_t)
+        // Step s handles column t = T-1-s.  Staged rows of step s are read BEFORE the step's
+        // barrier, so each tile is committed on the last step of the previous tile; the
+        // unrolled tile keeps the periodic work branch-free like the forward sweep.
         double bt[RJN];
 #pragma unroll
         for (int r = 0; r < RJN; ++r) bt[r] = jv[r] ? 1.0 : 0.0;
-        int buf = 0;
+        double* sink = p.sink + l;  // padded states store here (never read)
         wait_vmem_all();
-        for (int s = 0; s < T; ++s) {  // step s handles column t = T-1-s
-          const int t = T - 1 - s;
-          if (s >= TE && (s & (TE - 1)) == 0) {  // a new staged tile (and maybe obs tile)
-            ot.advance(s, tid);
-            stage_commit(s);
-            lds_barrier();
-            stage_issue(s);
-          }
-          double qv[RJN], ps = 0.0;
+        for (int s0 = 0; s0 < T; s0 += TE) {
 #pragma unroll
-          for (int r = 0; r < RJN; ++r) {
-            qv[r] = staged(AST, s, jr[r]) * bt[r];  // padded states: 0 * 0
-            ps += qv[r];
-          }
-          ps += dpp_f64<DPP_R8>(ps);  // the row's two target-state groups
-          if (row_leader) RED[buf * 64 + row16] = ps;
-          double* Xb = X + buf * (XS + 64);
-          const bool more = t > 0;
-          const bool rescale = (s & 7) == 0;
-          if (more) {
-            double v[RJN];
+          for (int sub = 0; sub < TE; ++sub) {
+            const int s = s0 + sub;
+            if (s < T) {
+              const int t = T - 1 - s;
+              const int buf = sub & 1;  // s0 is even
+              double* Xb = X + buf * (XS + 64);
+              double qv[RJN], v[RJN], ps = 0.0;
 #pragma unroll
-            for (int r = 0; r < RJN; ++r) v[r] = bt[r] * staged(EST, s, jr[r]);
+              for (int r = 0; r < RJN; ++r) {
+                qv[r] = staged(AST, s, jr[r]) * bt[r];  // padded states: 0 * 0
+                ps += qv[r];
+                v[r] = bt[r] * staged(EST, s, jr[r]);
+                Xb[jx[r]] = v[r];
+              }
+              ps += dpp_f64<DPP_R8>(ps);  // the row's two target-state groups
+              if (row_leader) RED[buf * 64 + row16] = ps;
+              const bool rescale = (sub & 7) == 0;
+              if (rescale) {
+                double mx = v[0];
 #pragma unroll
-            for (int r = 0; r < RJN; ++r) Xb[jx[r]] = v[r];
-            if (rescale) {
-              double mx = v[0];
+                for (int r = 1; r < RJN; ++r) mx = fmax(mx, v[r]);
+                mx = fmax(mx, dpp_f64<DPP_R8>(mx));
+                if (row_leader) RED[128 + buf * 64 + row16] = mx;
+              }
+              if (sub == 0) ot.advance(s, tid);
+              if (sub == TE - 1) stage_commit(s + 1);
+              lds_barrier();
+              if (sub == TE - 1) stage_issue(s + 1);
+              double S = 0.0;
 #pragma unroll
-              for (int r = 1; r < RJN; ++r) mx = fmax(mx, v[r]);
-              mx = fmax(mx, dpp_f64<DPP_R8>(mx));
-              if (row_leader) RED[128 + buf * 64 + row16] = mx;
+              for (int u = 0; u < NROW; ++u) S += RED[buf * 64 + u];
+              const double rS = 1.0 / S;
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) {
+                double* dst = jv[r] ? p.post + (c0 + t) * n + jr[r] : sink;
+                *dst = qv[r] * rS;
+              }
+              double sc = 1.0;
+              if (rescale) {
+                double M = RED[128 + buf * 64];
+#pragma unroll
+                for (int u = 1; u < NROW; ++u) M = fmax(M, RED[128 + buf * 64 + u]);
+                if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
+              }
+              const double* xs = Xb + q * IQS;
+              double acc[NCH][RJN];
+#pragma unroll
+              for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) acc[c][r] = 0.0;
+#pragma unroll
+              for (int k = 0; k < IQ; ++k) {
+                const double xi = xs[k];
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) acc[k % NCH][r] = fma(xi, m[k][r], acc[k % NCH][r]);
+              }
+              double sum[RJN];
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) {
+                sum[r] = acc[0][r];
+#pragma unroll
+                for (int c = 1; c < NCH; ++c) sum[r] += acc[c][r];
+              }
+              combine_sum(sum);
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) bt[r] = sum[r] * sc;
             }
           }
-          lds_barrier();
-          double S = 0.0;
-#pragma unroll
-          for (int u = 0; u < NROW; ++u) S += RED[buf * 64 + u];
-          if (q == 0) {
-#pragma unroll
-            for (int r = 0; r < RJN; ++r)
-              if (jv[r]) p.post[(c0 + t) * n + jr[r]] = qv[r] / S;
-          }
-          if (more) {
-            double sc = 1.0;
-            if (rescale) {
-              double M = RED[128 + buf * 64];
-#pragma unroll
-              for (int u = 1; u < NROW; ++u) M = fmax(M, RED[128 + buf * 64 + u]);
-              if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
-            }
-            double acc[RJN];
-#pragma unroll
-            for (int r = 0; r < RJN; ++r) acc[r] = 0.0;
-            const double* xs = Xb + q * IQS;
-#pragma unroll
-            for (int k = 0; k < IQ; ++k) {
-              const double xi = xs[k];
-#pragma unroll
-              for (int r = 0; r < RJN; ++r) acc[r] = fma(xi, m[k][r], acc[r]);
-            }
-            combine_sum(acc);
-#pragma unroll
-            for (int r = 0; r < RJN; ++r) bt[r] = acc[r] * sc;
-          }
-          buf ^= 1;
         }
       } else {
         // ------------- Viterbi (optimizer.py:305-333), back-pointers as uint8

@@ -25,6 +25,7 @@ struct SweepArgs {
   double* loglik;               // [nblocks]                       (MODE_FWD_LL)
   double* alpha;                // [total x XR] rescaled forward rows (FWD_STORE out, BWD in)
   double* post;                 // [total x n] posteriors          (MODE_BWD)
+  double* sink;                 // [64] write target of padded states (MODE_BWD)
   uint8_t* bp;                  // [total x XR] back-pointers      (MODE_VIT)
   uint8_t* chunk_map;           // [nchunks x XR] chunk origin maps (MODE_VIT)
   const int64_t* chunk_base;    // [nblocks] first chunk of each block
