@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -205,6 +206,9 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname) {
   if (grid > a.nblocks) grid = a.nblocks;
   if (grid <= 0) return 0;
   HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
+  if (getenv("ITR_VERBOSE"))
+    fprintf(stderr, "[itr] %s: n=%d cfg=%d block=%d lds=%zu per_cu=%d grid=%lld\n", tname, a.n,
+            g.iq, g.block, g.lds, g.per_cu, (long long)grid);
 #ifdef ITR_DIAG
   if (!g_diag) HIP_TRY(hipMalloc(&g_diag, 16 * sizeof(uint64_t)));
   HIP_TRY(hipMemsetAsync(g_diag, 0, 16 * sizeof(uint64_t), st));

@@ -46,7 +46,9 @@
 namespace itr {
 
 static constexpr int Q = 8;        // lanes splitting the i-sum of one target state
-static constexpr int TE = 16;      // columns per staged tile of per-column rows
+// columns per staged tile of per-column rows: 16, or 8 for the backward sweep of large
+// models (it stages two tables; 8 keeps two workgroups' LDS within the CU's 160 KiB)
+static constexpr int tile_cols(int mode, int xr) { return (mode == MODE_BWD && xr > 96) ? 8 : 16; }
 static constexpr double LN2 = 0.69314718055994530942;
 
 // Diagnostic build only (-DITR_DIAG, libitrails_hip_diag.so): wave 0 of every workgroup
@@ -215,11 +217,11 @@ struct ObsTiles {
 // column) for TE consecutive steps, loaded into registers one tile ahead and committed to an
 // LDS ring [2][TE][XR] at the tile boundary.  Element idx = tid + e*TB of a tile is row
 // idx / XR, target state idx % XR.
-template <int WV, int RJN>
+template <int WV, int RJN, int TE>
 struct RowStage {
   static constexpr int TB = 64 * WV;
   static constexpr int XR = WV * 8 * RJN;  // padded target states
-  static constexpr int RS = TE * XR / TB;  // = 2 * RJN elements per thread
+  static constexpr int RS = TE * XR / TB;  // = TE / 8 * RJN elements per thread
   static_assert(RS * TB == TE * XR, "tile must split evenly over the workgroup");
   double v[RS];
   template <class RowOf>
@@ -269,6 +271,7 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
   constexpr int XS = Q * IQS;         // published vector length
   constexpr int JW = 8 * RJN;         // target states per wave
   constexpr int XR = W * JW;          // padded target states per workgroup
+  constexpr int TE = tile_cols(MODE, XR);
   constexpr int NCH = IQ >= 6 ? 3 : (IQ >= 2 ? 2 : 1);  // independent chains per target
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int n = p.n;
@@ -320,8 +323,8 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
   for (int i = tid; i < 2 * (XS + 64); i += TB) X[i] = pad;
   lds_barrier();
 
-  RowStage<W, RJN> est;
-  RowStage<W, RJN> ast;
+  RowStage<W, RJN, TE> est;
+  RowStage<W, RJN, TE> ast;
   (void)ast;
   DIAG_DECL
 
@@ -814,7 +817,7 @@ static size_t lds_bytes(int cfg, int mode) {
   const int tb = 64 * w;
   const int stages = (mode == MODE_BWD) ? 2 : 1;
   return (size_t)2 * (xs + 64) * sizeof(double) + 5 * 64 * sizeof(double) +
-         (size_t)stages * 2 * TE * xr * sizeof(double) + 32 * sizeof(int) +
+         (size_t)stages * 2 * tile_cols(mode, xr) * xr * sizeof(double) + 32 * sizeof(int) +
          (size_t)2 * tb * sizeof(uint16_t) + 2 * (256 + 64);
 }
 
