@@ -56,6 +56,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="repeat the CPU-baseline sample until this much time has passed")
     ap.add_argument("--check", action="store_true", help="verify against the CPU oracle")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse the exchange with several ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -66,10 +69,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    cdev = dev if args.backend == "nccl" else torch.device("cpu")  # collective tensors
 
     from itrails_amd import hmm
     from itrails_amd.synth import block_lengths, sample_alignment
@@ -77,7 +85,9 @@ def main():
     a, b, pi, model_name = load_model(args.n_int)
     n = a.shape[0]
     cols = int(args.mbp * 1e6)
-    rng = np.random.default_rng(12345 + rank)
+    # identical block-length layout on every rank (weak scaling: the same work per GPU, so
+    # the makespan is not set by one rank drawing a longer tail block); content differs
+    rng = np.random.default_rng(12345)
     lengths = block_lengths(rng, cols, args.mean_block)
     t0 = time.time()
     obs, off, _ = sample_alignment(a, b, pi, lengths, seed=777 + rank)
@@ -93,13 +103,13 @@ def main():
     d_post = torch.empty((plan.total, n), dtype=torch.float64, device=dev) if post_mode else None
     nblk_global = plan.nblocks
     if world > 1:
-        counts = torch.tensor([plan.nblocks], device=dev)
+        counts = torch.tensor([plan.nblocks], device=cdev)
         allc = [torch.zeros_like(counts) for _ in range(world)]
         dist.all_gather(allc, counts)
         counts = [int(c.item()) for c in allc]
         nblk_global = sum(counts)
         first = sum(counts[:rank])
-        d_ll_global = torch.zeros(nblk_global, dtype=torch.float64, device=dev)
+        d_ll_global = torch.zeros(nblk_global, dtype=torch.float64, device=cdev)
 
     fwd_ms, vit_ms, tb_ms = [], [], []
 
@@ -118,7 +128,7 @@ def main():
             # each rank owns a disjoint slice of the global block vector: the all-reduce is
             # an exact gather (x + 0 = x), and the host sums in block order
             d_ll_global.zero_()
-            d_ll_global[first:first + plan.nblocks] = d_ll
+            d_ll_global[first:first + plan.nblocks] = d_ll.to(cdev)
             dist.all_reduce(d_ll_global)
         hmm.viterbi_device(model, plan, d_obs, out=d_path)
         if timing:
@@ -140,7 +150,7 @@ def main():
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     # kernel durations (HIP events on the launch stream), separate instrumented passes

@@ -582,13 +582,18 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
         // ------------- Viterbi (optimizer.py:305-333), back-pointers as uint8
         // Back-pointer rows and chunk maps have stride XR: every lane stores (duplicates
         // store the same byte, padded states a dummy one), no branches.
+        // Chunk origins (org_t[j] = state at column (chunk start - 1) on the best path into
+        // (t, j)) are resolved one step late: org_{t-1} = org_{t-2}[arg_{t-1}] is gathered
+        // after step t's barrier, where the LDS latency overlaps the max-plus chain, and
+        // published with x_{t} at step t+1.
         const int o0 = ot.get(0);
         double x[RJN];
-        int org[RJN];
+        int parg[RJN], porg[RJN];  // arg_{t-1}, org_{t-2}
 #pragma unroll
         for (int r = 0; r < RJN; ++r) {
           x[r] = jv[r] ? p.init[o0 * n + jr[r]] : -INFINITY;
-          org[r] = 0;
+          parg[r] = 0;
+          porg[r] = 0;
         }
         const int64_t cbase = p.chunk_base[blk];
         wait_vmem_all();
@@ -605,7 +610,7 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
 #pragma unroll
               for (int r = 0; r < RJN; ++r) {
                 Xb[jx[r]] = x[r];
-                Ob[jo[r]] = (uint8_t)org[r];
+                Ob[jo[r]] = (uint8_t)porg[r];
               }
               double ec[RJN];
               if (sub != 0) {
@@ -619,6 +624,9 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
               STAMP(0);
               lds_barrier();
               STAMP(1);
+              int og[RJN];  // org_{t-2}[arg_{t-1}]
+#pragma unroll
+              for (int r = 0; r < RJN; ++r) og[r] = Ob[parg[r]];
               if (sub == 0) {
                 stage_issue(t);
 #pragma unroll
@@ -669,27 +677,41 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
               combine_first_max(best, arg);
               STAMP(3);
               STAMP(4);
-              // chunk origin tracking: org = state at column (chunk start - 1) on the best
-              // path (VIT_CHUNK is a multiple of TE, so chunk boundaries fall on sub == 0)
-              const bool chunk_start = sub == 0 && (t % VIT_CHUNK) == 0;
+              // org_{t-1}: column t-1 starts a chunk -> its origin is arg_{t-1} itself
+              // (VIT_CHUNK is a multiple of TE: chunk starts fall on sub == 1, chunk ends
+              // of column t-1 on sub == 0)
 #pragma unroll
-              for (int r = 0; r < RJN; ++r) org[r] = chunk_start ? arg[r] : (int)Ob[arg[r]];
+              for (int r = 0; r < RJN; ++r)
+                porg[r] = (sub == 1 && ((t - 1) % VIT_CHUNK) == 0) ? parg[r] : og[r];
+              if (sub == 0 && (t % VIT_CHUNK) == 0 && t - 1 >= VIT_CHUNK) {
+                uint8_t* cm = p.chunk_map + (cbase + (t - 1) / VIT_CHUNK) * XR;
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) cm[jr[r]] = (uint8_t)porg[r];
+              }
               uint8_t* bprow = p.bp + (c0 + t) * XR;
 #pragma unroll
-              for (int r = 0; r < RJN; ++r) bprow[jr[r]] = (uint8_t)arg[r];
-              if (sub == TE - 1 || t == T - 1) {
-                const bool chunk_end = ((t + 1) % VIT_CHUNK) == 0 || t == T - 1;
-                if (chunk_end && t >= VIT_CHUNK) {
-                  uint8_t* cm = p.chunk_map + (cbase + t / VIT_CHUNK) * XR;
-#pragma unroll
-                  for (int r = 0; r < RJN; ++r) cm[jr[r]] = (uint8_t)org[r];
-                }
+              for (int r = 0; r < RJN; ++r) {
+                bprow[jr[r]] = (uint8_t)arg[r];
+                parg[r] = arg[r];
+                x[r] = best[r];  // padded states publish to the sink; never read
               }
-#pragma unroll
-              for (int r = 0; r < RJN; ++r) x[r] = jv[r] ? best[r] : -INFINITY;
               STAMP(5);
             }
           }
+        }
+        // org_{T-1} closes the last chunk: publish org_{T-2}, gather with arg_{T-1}
+        if (T - 1 >= VIT_CHUNK) {
+          uint8_t* Ob = ORIG + (T & 1) * (256 + 64);
+#pragma unroll
+          for (int r = 0; r < RJN; ++r) Ob[jo[r]] = (uint8_t)porg[r];
+        }
+        lds_barrier();
+        if (T - 1 >= VIT_CHUNK) {
+          const uint8_t* Ob = ORIG + (T & 1) * (256 + 64);
+          uint8_t* cm = p.chunk_map + (cbase + (T - 1) / VIT_CHUNK) * XR;
+          const bool cs = ((T - 1) % VIT_CHUNK) == 0;
+#pragma unroll
+          for (int r = 0; r < RJN; ++r) cm[jr[r]] = (uint8_t)(cs ? parg[r] : Ob[parg[r]]);
         }
         // last state = first argmax of omega_{T-1}  (optimizer.py:346)
         double bv = jv[0] ? x[0] : -INFINITY;
