@@ -213,6 +213,7 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname) {
   if (!g_diag) HIP_TRY(hipMalloc(&g_diag, 16 * sizeof(uint64_t)));
   HIP_TRY(hipMemsetAsync(g_diag, 0, 16 * sizeof(uint64_t), st));
   a.diag = g_diag;
+  a.diag_wave = getenv("ITR_DIAG_WAVE") ? atoi(getenv("ITR_DIAG_WAVE")) : 0;
 #endif
   {
     Scope sc(tname, st);

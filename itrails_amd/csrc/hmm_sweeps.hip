@@ -51,7 +51,7 @@ static constexpr int Q = 8;        // lanes splitting the i-sum of one target st
 static constexpr int tile_cols(int mode, int xr) { return (mode == MODE_BWD && xr > 96) ? 8 : 16; }
 static constexpr double LN2 = 0.69314718055994530942;
 
-// Diagnostic build only (-DITR_DIAG, libitrails_hip_diag.so): wave 0 of every workgroup
+// Diagnostic build only (-DITR_DIAG, libitrails_hip_diag.so): one wave (ITR_DIAG_WAVE, 0) of every workgroup
 // accumulates shader-clock cycles per step segment; never compiled into the product.
 #ifdef ITR_DIAG
 #define DIAG_DECL uint64_t dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t dlast = 0; uint64_t dsteps = 0;
@@ -66,7 +66,7 @@ static constexpr double LN2 = 0.69314718055994530942;
 #define DIAG_STEP() (++dsteps)
 #define DIAG_FLUSH()                                                          \
   do {                                                                        \
-    if (tid == 0 && p.diag) {                                                 \
+    if (l == 0 && w == p.diag_wave && p.diag) {                               \
       for (int i_ = 0; i_ < 8; ++i_) atomicAdd((unsigned long long*)&p.diag[i_], \
                                                (unsigned long long)dsum[i_]);  \
       atomicAdd((unsigned long long*)&p.diag[8], (unsigned long long)dsteps);   \

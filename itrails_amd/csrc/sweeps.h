@@ -32,6 +32,7 @@ struct SweepArgs {
   uint8_t* last_state;          // [nblocks] argmax of the last column (MODE_VIT)
   int prio_len;                 // blocks at least this long run at raised wave priority
   uint64_t* diag;               // diagnostic build only: per-segment cycle sums
+  int diag_wave;                // diagnostic build only: the wave that reports
 };
 
 struct SweepGeometry {

@@ -15,7 +15,7 @@ torch.cuda.set_device(0)
 model = hmm.Model(a, b, pi)
 names = {"fwd": ["pre-barrier", "barrier", "reads+fma", "combine", "mul", "post"],
          "vit": ["pre-barrier", "barrier", "reads+max", "combine", "tie/M", "post"]}
-tag = os.environ.get("ITR_SWEEP_CFG", "auto") + "/" + os.environ.get("ITR_PER_CU", "api")
+tag = os.environ.get("ITR_SWEEP_CFG", "auto") + "/" + os.environ.get("ITR_PER_CU", "api") + "/w" + os.environ.get("ITR_DIAG_WAVE", "0")
 for label, lengths in [("1x20000", [20000]), ("256x20000", [20000] * 256), ("768x5000", [5000] * 768)]:
     obs, off, _ = sample_alignment(a, b, pi, lengths, seed=1)
     plan = hmm.Plan(off)
@@ -27,6 +27,9 @@ for label, lengths in [("1x20000", [20000]), ("256x20000", [20000] * 256), ("768
         buf = np.zeros(16, dtype=np.uint64)
         _lib.check(L.itr_diag_read(buf.ctypes.data))
         steps = float(buf[8])
+        if steps == 0:
+            print(tag, label, kind, "no steps recorded by this wave", flush=True)
+            continue
         per = {names[kind][i]: round(float(buf[i]) / steps, 1) for i in range(6)}
         tot = sum(per.values())
         T = max(lengths)
