@@ -244,8 +244,9 @@ def pmc_traffic(n, mode=3):
             if name.startswith("void itr::sweep_kernel<") and name.endswith(f", {mode}>(itr::SweepArgs)") \
                     and v.get("n_states", 70) == n and "hbm_bytes_raw" in v:
                 return round(v["hbm_bytes_raw"]), (
-                    f"{os.path.basename(f)}: FETCH_SIZE+WRITE_SIZE per launch (raw; "
-                    "writes are the uint8 back-pointer rows, stride 96 B/column)")
+                    f"{os.path.basename(f)} ({name}): FETCH_SIZE+WRITE_SIZE per launch, raw; "
+                    "Viterbi writes are the uint8 back-pointer rows (padded-state stride), "
+                    "posterior writes the f64 rows")
     return None, "no PMC summary under profiles/"
 
 
