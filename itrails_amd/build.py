@@ -10,6 +10,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["hmm_sweeps.hip", "dense.hip", "emission.hip", "maf.cpp", "writers.cpp", "capi.cpp"]
 OUT = os.path.join(HERE, "libitrails_hip.so")
+# The sweeps never produce NaN (log 0 = -inf is the only non-finite value, and no
+# inf - inf or 0/0 is formed), so fmax needs no NaN-quieting canonicalize after each DPP
+# move; infinities keep their IEEE semantics (no -ffinite-math-only).
+EXTRA = {"hmm_sweeps.hip": ["-fno-honor-nans"]}
 ARCH = os.environ.get("ITR_OFFLOAD_ARCH", "gfx950")
 
 
@@ -35,7 +39,7 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
     objs, procs = [], []
     for src in SOURCES:  # one compiler per translation unit, in parallel
         obj = os.path.join(CSRC, "..", f".{os.path.splitext(src)[0]}{tag}.o")
-        cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [hipcc] + flags + EXTRA.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append(subprocess.Popen(cmd))

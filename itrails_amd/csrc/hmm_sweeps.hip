@@ -147,12 +147,17 @@ __device__ __forceinline__ void combine_first_max(double (&best)[RJN], int (&arg
   int a[RJN];
 #pragma unroll
   for (int r = 0; r < RJN; ++r) a[r] = (best[r] == mx[r]) ? arg[r] : 0x7fffffff;
+  // update_dpp with the identity of min as `old` lets the DPP-combine pass fold each
+  // mov into the v_min_i32 (one instruction per stage)
 #pragma unroll
-  for (int r = 0; r < RJN; ++r) a[r] = min(a[r], dpp_i32<DPP_Q1>(a[r]));
+  for (int r = 0; r < RJN; ++r)
+    a[r] = min(a[r], __builtin_amdgcn_update_dpp(0x7fffffff, a[r], DPP_Q1, 0xF, 0xF, false));
 #pragma unroll
-  for (int r = 0; r < RJN; ++r) a[r] = min(a[r], dpp_i32<DPP_Q2>(a[r]));
+  for (int r = 0; r < RJN; ++r)
+    a[r] = min(a[r], __builtin_amdgcn_update_dpp(0x7fffffff, a[r], DPP_Q2, 0xF, 0xF, false));
 #pragma unroll
-  for (int r = 0; r < RJN; ++r) a[r] = min(a[r], dpp_i32<DPP_HM>(a[r]));
+  for (int r = 0; r < RJN; ++r)
+    a[r] = min(a[r], __builtin_amdgcn_update_dpp(0x7fffffff, a[r], DPP_HM, 0xF, 0xF, false));
 #pragma unroll
   for (int r = 0; r < RJN; ++r) {
     best[r] = mx[r];
