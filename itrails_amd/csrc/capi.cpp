@@ -115,18 +115,16 @@ struct itr_model {
 
 struct itr_plan {
   int device = 0;
-  int64_t nblocks = 0, total = 0, nchunks = 0;
-  int64_t *d_off = nullptr, *d_chunk_base = nullptr;
-  int32_t *d_order = nullptr, *d_chunk_blk = nullptr;
-  int* d_queue = nullptr;
+  int64_t nblocks = 0, total = 0;
+  int64_t* d_off = nullptr;
+  int32_t* d_order = nullptr;
+  int* d_queue = nullptr;  // [0] sweep work counter, [1] traceback work counter
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
-  // workspace (grown on demand)
-  uint8_t* d_bp = nullptr;
-  size_t bp_cap = 0;
-  uint8_t* d_chunk_map = nullptr;
-  size_t cm_cap = 0;
-  uint8_t* d_chunk_end = nullptr;
+  // workspace (grown on demand): forward rows (posterior) or omega rows (Viterbi), and the
+  // Viterbi stay flags
+  uint8_t* d_stay = nullptr;
+  size_t stay_cap = 0;
   uint8_t* d_last = nullptr;
   double* d_alpha = nullptr;
   size_t alpha_cap = 0;
@@ -151,31 +149,29 @@ int check_plan(itr_plan_t p) {
   return 0;
 }
 
+// row stride of the Viterbi stay flags: columns rounded up, plus slack so a 64-column
+// window never leaves the row
+int64_t stay_stride(int64_t total) { return ((total + 63) / 64) * 64 + 64; }
+
 int reserve(itr_plan_t p, int n, bool vit, bool post) {
   const int xr = itr::sweep_row_stride(n, itr::MODE_VIT);
   const int xa = itr::sweep_row_stride(n, itr::MODE_BWD);
   if (xr < 0 || xa < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", n);
+  size_t need_rows = 0;
   if (vit) {
-    const size_t need = (size_t)p->total * xr;
-    if (need > p->bp_cap) {
-      dev_free(p->d_bp);
-      if (int e = dev_alloc(&p->d_bp, need)) return e;
-      p->bp_cap = need;
-    }
-    const size_t needc = (size_t)p->nchunks * xr;
-    if (needc > p->cm_cap) {
-      dev_free(p->d_chunk_map);
-      if (int e = dev_alloc(&p->d_chunk_map, needc)) return e;
-      p->cm_cap = needc;
+    need_rows = (size_t)p->total * xr;
+    const size_t need = (size_t)n * stay_stride(p->total);
+    if (need > p->stay_cap) {
+      dev_free(p->d_stay);
+      if (int e = dev_alloc(&p->d_stay, need)) return e;
+      p->stay_cap = need;
     }
   }
-  if (post) {
-    const size_t need = (size_t)p->total * xa;
-    if (need > p->alpha_cap) {
-      dev_free(p->d_alpha);
-      if (int e = dev_alloc(&p->d_alpha, need)) return e;
-      p->alpha_cap = need;
-    }
+  if (post) need_rows = std::max(need_rows, (size_t)p->total * xa);
+  if (need_rows > p->alpha_cap) {
+    dev_free(p->d_alpha);
+    if (int e = dev_alloc(&p->d_alpha, need_rows)) return e;
+    p->alpha_cap = need_rows;
   }
   return 0;
 }
@@ -189,7 +185,6 @@ itr::SweepArgs base_args(itr_model_t m, itr_plan_t p, const uint16_t* obs) {
   a.queue = p->d_queue;
   a.sink = p->d_sink;
   a.obs = obs;
-  a.chunk_base = p->d_chunk_base;
   a.prio_len = p->prio_len;
   return a;
 }
@@ -309,18 +304,6 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
     return h_off[x + 1] - h_off[x] > h_off[y + 1] - h_off[y];
   });
-  // traceback chunks
-  std::vector<int64_t> cbase(nblocks);
-  std::vector<int32_t> cblk;
-  int64_t nc = 0;
-  for (int64_t k = 0; k < nblocks; ++k) {
-    cbase[k] = nc;
-    const int64_t T = h_off[k + 1] - h_off[k];
-    const int64_t K = (T + itr::VIT_CHUNK - 1) / itr::VIT_CHUNK;
-    for (int64_t c = 0; c < K; ++c) cblk.push_back((int32_t)k);
-    nc += K;
-  }
-  p->nchunks = nc;
   if (nblocks > 0) {
     const int64_t k = std::min<int64_t>(nblocks - 1, 255);
     const int64_t T = h_off[order[k] + 1] - h_off[order[k]];
@@ -329,11 +312,8 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   int e = 0;
   if (!e) e = dev_alloc(&p->d_off, nblocks + 1);
   if (!e) e = dev_alloc(&p->d_order, nblocks);
-  if (!e) e = dev_alloc(&p->d_chunk_base, nblocks);
-  if (!e) e = dev_alloc(&p->d_chunk_blk, nc);
   if (!e) e = dev_alloc(&p->d_queue, 4);
   if (!e) e = dev_alloc(&p->d_sink, 64);
-  if (!e) e = dev_alloc(&p->d_chunk_end, nc);
   if (!e) e = dev_alloc(&p->d_last, nblocks);
   auto up = [&](void* d, const void* h, size_t bytes) {
     if (e || bytes == 0) return;
@@ -342,8 +322,6 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   };
   up(p->d_off, h_off.data(), (nblocks + 1) * sizeof(int64_t));
   up(p->d_order, order.data(), nblocks * sizeof(int32_t));
-  up(p->d_chunk_base, cbase.data(), nblocks * sizeof(int64_t));
-  up(p->d_chunk_blk, cblk.data(), nc * sizeof(int32_t));
   if (e) {
     itr_plan_destroy(p);
     return e;
@@ -356,13 +334,9 @@ int itr_plan_destroy(itr_plan_t p) {
   if (!p) return 0;
   dev_free(p->d_off);
   dev_free(p->d_order);
-  dev_free(p->d_chunk_base);
-  dev_free(p->d_chunk_blk);
   dev_free(p->d_queue);
   dev_free(p->d_sink);
-  dev_free(p->d_bp);
-  dev_free(p->d_chunk_map);
-  dev_free(p->d_chunk_end);
+  dev_free(p->d_stay);
   dev_free(p->d_last);
   dev_free(p->d_alpha);
   delete p;
@@ -408,14 +382,31 @@ int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
   a.mat = m->la;
   a.emit = m->LE;
   a.init = m->LPIE;
-  a.bp = p->d_bp;
-  a.chunk_map = p->d_chunk_map;
+  a.alpha = p->d_alpha;
+  a.stay = p->d_stay;
+  a.fs = stay_stride(p->total);
   a.last_state = p->d_last;
   if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
+  itr::TraceArgs ta{};
+  ta.n = m->n;
+  ta.xr = itr::sweep_row_stride(m->n, itr::MODE_VIT);
+  ta.fs = a.fs;
+  ta.nblocks = p->nblocks;
+  ta.off = p->d_off;
+  ta.order = p->d_order;
+  ta.queue = p->d_queue + 1;
+  ta.obs = obs;
+  ta.log_a = m->la;
+  ta.log_e = m->LE;
+  ta.omega = p->d_alpha;
+  ta.stay = p->d_stay;
+  ta.last_state = p->d_last;
+  ta.path = path;
+  // one wave per block, 4 waves per workgroup
+  const int64_t grid = std::min<int64_t>((p->nblocks + 3) / 4, (int64_t)cu_count() * 8);
+  HIP_TRY(hipMemsetAsync(ta.queue, 0, sizeof(int), st));
   Scope sc("traceback", st);
-  HIP_TRY(itr::launch_vit_traceback(m->n, p->nblocks, p->nchunks, p->d_off, p->d_chunk_base,
-                                    p->d_chunk_blk, p->d_chunk_map, p->d_last, p->d_chunk_end,
-                                    p->d_bp, path, st));
+  HIP_TRY(itr::launch_vit_traceback(ta, (int)grid, st));
   return 0;
 }
 

@@ -130,39 +130,16 @@ __device__ __forceinline__ void combine_sum(double (&acc)[RJN]) {
 #pragma unroll
   for (int r = 0; r < RJN; ++r) acc[r] += dpp_f64<DPP_HM>(acc[r]);
 }
-// First maximum over the 8 lanes of a target state.  The maximum value is reduced first
-// (fmax is exact and order-free), then the winning index is the smallest arg among the
-// lanes whose own maximum equals it: lanes hold increasing i ranges and each lane's arg is
-// already its first maximum, so the minimum such arg is the first maximum overall.
-// All 8 lanes end with identical (best, arg).
+// Maximum over the 8 lanes of a target state (fmax is exact and order-free, so all 8 lanes
+// end with the identical value).
 template <int RJN>
-__device__ __forceinline__ void combine_first_max(double (&best)[RJN], int (&arg)[RJN]) {
-  double mx[RJN];
+__device__ __forceinline__ void combine_max(double (&v)[RJN]) {
 #pragma unroll
-  for (int r = 0; r < RJN; ++r) mx[r] = fmax(best[r], dpp_f64<DPP_Q1>(best[r]));
+  for (int r = 0; r < RJN; ++r) v[r] = fmax(v[r], dpp_f64<DPP_Q1>(v[r]));
 #pragma unroll
-  for (int r = 0; r < RJN; ++r) mx[r] = fmax(mx[r], dpp_f64<DPP_Q2>(mx[r]));
+  for (int r = 0; r < RJN; ++r) v[r] = fmax(v[r], dpp_f64<DPP_Q2>(v[r]));
 #pragma unroll
-  for (int r = 0; r < RJN; ++r) mx[r] = fmax(mx[r], dpp_f64<DPP_HM>(mx[r]));
-  int a[RJN];
-#pragma unroll
-  for (int r = 0; r < RJN; ++r) a[r] = (best[r] == mx[r]) ? arg[r] : 0x7fffffff;
-  // update_dpp with the identity of min as `old` lets the DPP-combine pass fold each
-  // mov into the v_min_i32 (one instruction per stage)
-#pragma unroll
-  for (int r = 0; r < RJN; ++r)
-    a[r] = min(a[r], __builtin_amdgcn_update_dpp(0x7fffffff, a[r], DPP_Q1, 0xF, 0xF, false));
-#pragma unroll
-  for (int r = 0; r < RJN; ++r)
-    a[r] = min(a[r], __builtin_amdgcn_update_dpp(0x7fffffff, a[r], DPP_Q2, 0xF, 0xF, false));
-#pragma unroll
-  for (int r = 0; r < RJN; ++r)
-    a[r] = min(a[r], __builtin_amdgcn_update_dpp(0x7fffffff, a[r], DPP_HM, 0xF, 0xF, false));
-#pragma unroll
-  for (int r = 0; r < RJN; ++r) {
-    best[r] = mx[r];
-    arg[r] = a[r];
-  }
+  for (int r = 0; r < RJN; ++r) v[r] = fmax(v[r], dpp_f64<DPP_HM>(v[r]));
 }
 
 // s_waitcnt vmcnt(0) (expcnt/lgkmcnt untouched).  Issued once before each step loop so
@@ -297,11 +274,10 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
   int* SBLK = reinterpret_cast<int*>(AST + ((MODE == MODE_BWD) ? 2 * TE * XR : 0));
   int* REDI = SBLK + 4;                                      // [16]
   uint16_t* OBS = reinterpret_cast<uint16_t*>(SBLK + 32);    // [2][TB]
-  uint8_t* ORIG = reinterpret_cast<uint8_t*>(OBS + 2 * TB);  // [2][256+64] (Viterbi)
 
   // Publishing is branch-free: the one lane (q == 0) of a real target state writes its
   // slot, every other lane writes the same value into its own sink entry nobody reads.
-  int jr[RJN], jx[RJN], jo[RJN];
+  int jr[RJN], jx[RJN];
   bool jv[RJN];
 #pragma unroll
   for (int r = 0; r < RJN; ++r) {
@@ -309,17 +285,25 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
     jv[r] = jr[r] < n;
     const bool pub = jv[r] && q == 0;
     jx[r] = pub ? (jr[r] / IQ) * IQS + jr[r] % IQ : XS + l;  // slot of state jr in X
-    jo[r] = pub ? jr[r] : 256 + l;                            // slot of state jr in ORIG
   }
 
-  // this lane's slice of a (or log a): rows i = q*IQ + k, columns jr[r]
+  // this lane's slice of a (or log a): rows i = q*IQ + k, columns jr[r].  Viterbi keeps the
+  // self-transition log a_jj out of the max-plus chain (-inf there) and in ldiag instead:
+  // the chain then yields max over i != j, which with the diagonal term decides whether
+  // the first maximum is j itself (see the Viterbi sweep below).
   double m[IQ][RJN];
+  double ldiag[RJN];
+#pragma unroll
+  for (int r = 0; r < RJN; ++r)
+    ldiag[r] = (MODE == MODE_VIT && jv[r]) ? p.mat[(int64_t)jr[r] * n + jr[r]] : 0.0;
 #pragma unroll
   for (int k = 0; k < IQ; ++k) {
     const int i = q * IQ + k;
 #pragma unroll
-    for (int r = 0; r < RJN; ++r)
+    for (int r = 0; r < RJN; ++r) {
       m[k][r] = (i < n && jv[r]) ? p.mat[(int64_t)i * n + jr[r]] : 0.0;
+      if (MODE == MODE_VIT && i == jr[r]) m[k][r] = -INFINITY;
+    }
   }
 
   // published entries of states >= n are never written: 0 for the probability sweeps
@@ -584,23 +568,27 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
           }
         }
       } else {
-        // ------------- Viterbi (optimizer.py:305-333), back-pointers as uint8
-        // Back-pointer rows and chunk maps have stride XR: every lane stores (duplicates
-        // store the same byte, padded states a dummy one), no branches.
-        // Chunk origins (org_t[j] = state at column (chunk start - 1) on the best path into
-        // (t, j)) are resolved one step late: org_{t-1} = org_{t-2}[arg_{t-1}] is gathered
-        // after step t's barrier, where the LDS latency overlaps the max-plus chain, and
-        // published with x_{t} at step t+1.
+        // ------------- Viterbi (optimizer.py:305-333)
+        //   omega_t[j] = max_i (omega_{t-1}[i] + log a_ij) + log e_j,  bp = first argmax.
+        // Rounding is monotone, so max_i fl(z_i + c) = fl(max_i z_i + c): the chain takes
+        // the max of z_i = omega_i + log a_ij over i != j (one add + one max per pair), the
+        // diagonal z_j = omega_j + log a_jj is formed separately, and
+        //   yd = fl(z_j + c), yo = fl(max_{i != j} z_i + c), omega_t[j] = max(yd, yo)
+        // is bit-identical to the reference's value.  yd > yo means j is the unique maximum,
+        // so bp(t, j) = j for certain: that is the stay flag.  Otherwise (a switch, or a tie
+        // the first-max rule must break) the traceback recomputes bp(t, j) exactly from the
+        // stored omega rows.  Rows (stride XR) and flags (state-major, stride fs) are stored
+        // by the q == 0 lane of each real state.
         const int o0 = ot.get(0);
         double x[RJN];
-        int parg[RJN], porg[RJN];  // arg_{t-1}, org_{t-2}
 #pragma unroll
         for (int r = 0; r < RJN; ++r) {
           x[r] = jv[r] ? p.init[o0 * n + jr[r]] : -INFINITY;
-          parg[r] = 0;
-          porg[r] = 0;
+          if (q == 0 && jv[r]) p.alpha[c0 * XR + jr[r]] = x[r];
         }
-        const int64_t cbase = p.chunk_base[blk];
+        uint8_t* stay_row[RJN];
+#pragma unroll
+        for (int r = 0; r < RJN; ++r) stay_row[r] = p.stay + (int64_t)jr[r] * p.fs + c0;
         wait_vmem_all();
         STAMP(-1);
         for (int t0 = 0; t0 < T; t0 += TE) {
@@ -611,12 +599,8 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
               DIAG_STEP();
               const int buf = sub & 1;  // t0 is even
               double* Xb = X + buf * (XS + 64);
-              uint8_t* Ob = ORIG + buf * (256 + 64);
 #pragma unroll
-              for (int r = 0; r < RJN; ++r) {
-                Xb[jx[r]] = x[r];
-                Ob[jo[r]] = (uint8_t)porg[r];
-              }
+              for (int r = 0; r < RJN; ++r) Xb[jx[r]] = x[r];
               double ec[RJN];
               if (sub != 0) {
 #pragma unroll
@@ -629,94 +613,57 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
               STAMP(0);
               lds_barrier();
               STAMP(1);
-              int og[RJN];  // org_{t-2}[arg_{t-1}]
-#pragma unroll
-              for (int r = 0; r < RJN; ++r) og[r] = Ob[parg[r]];
               if (sub == 0) {
                 stage_issue(t);
 #pragma unroll
                 for (int r = 0; r < RJN; ++r) ec[r] = staged(EST, t, jr[r]);
               }
               const double* xs = Xb + q * IQS;
-              // NCH independent first-max chains per target (k = c mod NCH, ascending),
-              // then merged: max value, and the smallest index among the chains holding it.
-              // Every candidate is the reference's exact value (omega_i + log a_ij) + log e_j
-              // (optimizer.py:326-330), so the first maximum is the reference's argmax.
+              // NCH independent max chains per target (k = c mod NCH)
               double bc[NCH][RJN];
-              int ac[NCH][RJN];
 #pragma unroll
               for (int c = 0; c < NCH; ++c) {
                 const double xc = xs[c];
 #pragma unroll
-                for (int r = 0; r < RJN; ++r) {
-                  bc[c][r] = (xc + m[c][r]) + ec[r];
-                  ac[c][r] = c;
-                }
+                for (int r = 0; r < RJN; ++r) bc[c][r] = xc + m[c][r];
               }
 #pragma unroll
               for (int k = NCH; k < IQ; ++k) {
                 const double xi = xs[k];
 #pragma unroll
-                for (int r = 0; r < RJN; ++r) {
-                  const double y = (xi + m[k][r]) + ec[r];
-                  const bool gt = y > bc[k % NCH][r];
-                  bc[k % NCH][r] = fmax(bc[k % NCH][r], y);
-                  ac[k % NCH][r] = gt ? k : ac[k % NCH][r];
-                }
+                for (int r = 0; r < RJN; ++r) bc[k % NCH][r] = fmax(bc[k % NCH][r], xi + m[k][r]);
               }
-              double best[RJN];
-              int arg[RJN];
+              double zo[RJN];
 #pragma unroll
               for (int r = 0; r < RJN; ++r) {
-                double b = bc[0][r];
+                zo[r] = bc[0][r];
 #pragma unroll
-                for (int c = 1; c < NCH; ++c) b = fmax(b, bc[c][r]);
-                int a = 0x7fffffff;
-#pragma unroll
-                for (int c = 0; c < NCH; ++c) a = (bc[c][r] == b) ? min(a, ac[c][r]) : a;
-                best[r] = b;
-                arg[r] = a + q * IQ;
+                for (int c = 1; c < NCH; ++c) zo[r] = fmax(zo[r], bc[c][r]);
               }
               STAMP(2);
-              // combine the 8 i-ranges; on equal maxima the lower range (lower i) wins
-              combine_first_max(best, arg);
+              combine_max(zo);  // max over i != j, identical in the 8 lanes
               STAMP(3);
-              STAMP(4);
-              // org_{t-1}: column t-1 starts a chunk -> its origin is arg_{t-1} itself
-              // (VIT_CHUNK is a multiple of TE: chunk starts fall on sub == 1, chunk ends
-              // of column t-1 on sub == 0)
-#pragma unroll
-              for (int r = 0; r < RJN; ++r)
-                porg[r] = (sub == 1 && ((t - 1) % VIT_CHUNK) == 0) ? parg[r] : og[r];
-              if (sub == 0 && (t % VIT_CHUNK) == 0 && t - 1 >= VIT_CHUNK) {
-                uint8_t* cm = p.chunk_map + (cbase + (t - 1) / VIT_CHUNK) * XR;
-#pragma unroll
-                for (int r = 0; r < RJN; ++r) cm[jr[r]] = (uint8_t)porg[r];
-              }
-              uint8_t* bprow = p.bp + (c0 + t) * XR;
+              bool st[RJN];
 #pragma unroll
               for (int r = 0; r < RJN; ++r) {
-                bprow[jr[r]] = (uint8_t)arg[r];
-                parg[r] = arg[r];
-                x[r] = best[r];  // padded states publish to the sink; never read
+                const double yd = (x[r] + ldiag[r]) + ec[r];
+                const double yo = zo[r] + ec[r];
+                st[r] = yd > yo;
+                x[r] = fmax(yd, yo);
+              }
+              STAMP(4);
+              if (q == 0) {
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) {
+                  if (jv[r]) {
+                    p.alpha[(c0 + t) * XR + jr[r]] = x[r];
+                    stay_row[r][t] = (uint8_t)st[r];
+                  }
+                }
               }
               STAMP(5);
             }
           }
-        }
-        // org_{T-1} closes the last chunk: publish org_{T-2}, gather with arg_{T-1}
-        if (T - 1 >= VIT_CHUNK) {
-          uint8_t* Ob = ORIG + (T & 1) * (256 + 64);
-#pragma unroll
-          for (int r = 0; r < RJN; ++r) Ob[jo[r]] = (uint8_t)porg[r];
-        }
-        lds_barrier();
-        if (T - 1 >= VIT_CHUNK) {
-          const uint8_t* Ob = ORIG + (T & 1) * (256 + 64);
-          uint8_t* cm = p.chunk_map + (cbase + (T - 1) / VIT_CHUNK) * XR;
-          const bool cs = ((T - 1) % VIT_CHUNK) == 0;
-#pragma unroll
-          for (int r = 0; r < RJN; ++r) cm[jr[r]] = (uint8_t)(cs ? parg[r] : Ob[parg[r]]);
         }
         // last state = first argmax of omega_{T-1}  (optimizer.py:346)
         double bv = jv[0] ? x[0] : -INFINITY;
@@ -756,49 +703,77 @@ __global__ void __launch_bounds__(64 * WV, (Occ<WV, RJN, IQ, MODE>::value))
 }
 
 // ---------------------------------------------------------------------------------------
-// Viterbi traceback (optimizer.py:336-354), chunked so that no thread chases more than
-// VIT_CHUNK pointers:
-//   chain: per block, walk the per-chunk maps from the last state to find every chunk's
-//          end state (ceil(T/C) hops);
-//   fill:  per chunk, chase the back-pointers from its end state (<= C hops).
+// Viterbi traceback (optimizer.py:336-354) over the omega rows and stay flags of MODE_VIT.
+// One wave per block (longest first from a work counter).  Walking down from the last
+// column with the current state s, the path stays in s as long as stay(t, s) holds, so the
+// wave reads s's flag row 256 columns per round trip (four 64-column windows in flight,
+// lane l on column t - 64w - l), writes the run of s in one store per window, and stops at
+// the first column whose flag is clear.  There it evaluates the reference's expression
+// for every i — (omega_{t-1}[i] + log a_is) + log e_s(t), lane i (+64, +128) — and takes
+// the first i equal to omega_t[s] (ballot, lowest set bit): that is np.argmax's first
+// maximum, because omega_t[s] is by construction the maximum of exactly these values.
 // ---------------------------------------------------------------------------------------
-__global__ void vit_chain_kernel(int xr, int64_t nblocks, const int64_t* __restrict__ off,
-                                 const int64_t* __restrict__ chunk_base,
-                                 const uint8_t* __restrict__ chunk_map,
-                                 const uint8_t* __restrict__ last_state,
-                                 uint8_t* __restrict__ chunk_end) {
-  const int64_t blk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (blk >= nblocks) return;
-  const int64_t T = off[blk + 1] - off[blk];
-  if (T <= 0) return;
-  const int64_t cb = chunk_base[blk];
-  const int64_t K = (T + VIT_CHUNK - 1) / VIT_CHUNK;
-  int s = last_state[blk];
-  chunk_end[cb + K - 1] = (uint8_t)s;
-  for (int64_t k = K - 1; k >= 1; --k) {
-    s = chunk_map[(cb + k) * xr + s];
-    chunk_end[cb + k - 1] = (uint8_t)s;
+template <int G>  // state groups of 64 lanes: n <= 64 G
+__device__ __forceinline__ int vit_bp(const TraceArgs& p, int64_t c0, int t, int s, int l) {
+  const int64_t col = c0 + t;
+  const int sym = min((int)p.obs[col], 624);
+  const double le = p.log_e[(int64_t)sym * p.n + s];
+  const double M = p.omega[col * p.xr + s];
+  const double* row = p.omega + (col - 1) * p.xr;
+  int res = -1;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int i = l + 64 * g;
+    double y = -INFINITY;
+    if (i < p.n) y = (row[i] + p.log_a[(int64_t)i * p.n + s]) + le;
+    const uint64_t hit = __ballot(y == M);
+    if (res < 0 && hit) res = 64 * g + __builtin_ctzll(hit);
   }
+  return res < 0 ? 0 : res;  // unreachable: omega_t[s] is one of the y
 }
 
-__global__ void vit_fill_kernel(int xr, int64_t nchunks, const int64_t* __restrict__ off,
-                                const int64_t* __restrict__ chunk_base,
-                                const int32_t* __restrict__ chunk_blk,
-                                const uint8_t* __restrict__ chunk_end,
-                                const uint8_t* __restrict__ bp, uint8_t* __restrict__ path) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= nchunks) return;
-  const int blk = chunk_blk[c];
-  const int64_t c0 = off[blk];
-  const int64_t T = off[blk + 1] - c0;
-  const int64_t k = c - chunk_base[blk];
-  const int64_t lo = k * VIT_CHUNK;
-  const int64_t hi = (lo + VIT_CHUNK < T) ? lo + VIT_CHUNK : T;
-  int s = chunk_end[c];
-  path[c0 + hi - 1] = (uint8_t)s;
-  for (int64_t t = hi - 1; t > lo; --t) {
-    s = bp[(c0 + t) * xr + s];
-    path[c0 + t - 1] = (uint8_t)s;
+template <int G>
+__global__ void __launch_bounds__(256) vit_trace_kernel(TraceArgs p) {
+  const int l = threadIdx.x & 63;
+  for (;;) {
+    int bi = 0;
+    if (l == 0) bi = atomicAdd(p.queue, 1);
+    bi = uni(__shfl(bi, 0));
+    if (bi >= p.nblocks) break;
+    const int blk = uni(p.order[bi]);
+    const int64_t c0 = p.off[blk];
+    const int T = uni((int)(p.off[blk + 1] - c0));
+    if (T <= 0) continue;  // no barrier in this kernel: a wave-uniform continue is safe
+    uint8_t* path = p.path + c0;
+    int s = uni((int)p.last_state[blk]);
+    if (l == 0) path[T - 1] = (uint8_t)s;
+    int t = T - 1;  // column whose state (s) is known
+    while (t >= 1) {
+      const uint8_t* fr = p.stay + (int64_t)s * p.fs + c0;
+      int f[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int u = t - 64 * w - l;
+        f[w] = (u >= 1) ? (int)fr[u] : 1;
+      }
+      const int tb = t;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int top = tb - 64 * w;
+        if (top < 1) break;
+        const uint64_t clear = __ballot(f[w] == 0 && top - l >= 1);
+        const int nvalid = min(64, top);
+        const int run = clear ? __builtin_ctzll(clear) : nvalid;  // stay columns on top
+        if (l < run) path[top - l - 1] = (uint8_t)s;
+        t = top - run;
+        if (clear) {  // column t: switch or tie, resolve exactly
+          s = uni(vit_bp<G>(p, c0, t, s, l));
+          if (l == 0) path[t - 1] = (uint8_t)s;
+          t -= 1;
+          break;  // the windows still in registers belong to the old state
+        }
+      }
+    }
   }
 }
 
@@ -845,7 +820,7 @@ static size_t lds_bytes(int cfg, int mode) {
   const int stages = (mode == MODE_BWD) ? 2 : 1;
   return (size_t)2 * (xs + 64) * sizeof(double) + 5 * 64 * sizeof(double) +
          (size_t)stages * 2 * tile_cols(mode, xr) * xr * sizeof(double) + 32 * sizeof(int) +
-         (size_t)2 * tb * sizeof(uint16_t) + 2 * (256 + 64);
+         (size_t)2 * tb * sizeof(uint16_t);
 }
 
 template <int WV, int RJN, int IQ, int MODE>
@@ -927,27 +902,17 @@ int sweep_row_stride(int n, int mode) {  // padded target states: row stride of 
   return c < 0 ? -1 : 8 * kCfgs[c].w * kCfgs[c].rj;
 }
 
-hipError_t launch_vit_traceback(int n, int64_t nblocks, int64_t nchunks, const int64_t* off,
-                                const int64_t* chunk_base, const int32_t* chunk_blk,
-                                const uint8_t* chunk_map, const uint8_t* last_state,
-                                uint8_t* chunk_end, const uint8_t* bp, uint8_t* path,
-                                hipStream_t st) {
-  if (nblocks > 0) {
-    const int tb = 256;
-    hipLaunchKernelGGL(vit_chain_kernel, dim3((unsigned)((nblocks + tb - 1) / tb)), dim3(tb),
-                       0, st, sweep_row_stride(n, MODE_VIT), nblocks, off, chunk_base, chunk_map, last_state,
-                       chunk_end);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+hipError_t launch_vit_traceback(const TraceArgs& a, int grid, hipStream_t st) {
+  if (a.nblocks <= 0) return hipSuccess;
+  const int g = (a.n + 63) / 64;
+  switch (g) {
+    case 1: hipLaunchKernelGGL(vit_trace_kernel<1>, dim3(grid), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(vit_trace_kernel<2>, dim3(grid), dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(vit_trace_kernel<3>, dim3(grid), dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL(vit_trace_kernel<4>, dim3(grid), dim3(256), 0, st, a); break;
+    default: return hipErrorInvalidValue;
   }
-  if (nchunks > 0) {
-    const int tb = 256;
-    hipLaunchKernelGGL(vit_fill_kernel, dim3((unsigned)((nchunks + tb - 1) / tb)), dim3(tb), 0,
-                       st, sweep_row_stride(n, MODE_VIT), nchunks, off, chunk_base, chunk_blk, chunk_end, bp,
-                       path);
-    return hipGetLastError();
-  }
-  return hipSuccess;
+  return hipGetLastError();
 }
 
 }  // namespace itr

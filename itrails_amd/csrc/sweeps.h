@@ -8,9 +8,6 @@ namespace itr {
 
 enum SweepMode { MODE_FWD_LL = 0, MODE_FWD_STORE = 1, MODE_BWD = 2, MODE_VIT = 3 };
 
-// columns per Viterbi traceback chunk (bounds every pointer chase)
-static constexpr int VIT_CHUNK = 256;
-
 struct SweepArgs {
   int n;                        // hidden states
   int xp;                       // padded length of the LDS state vectors
@@ -23,12 +20,12 @@ struct SweepArgs {
   const double* emit;           // E or log E, 625 x n
   const double* init;           // pi*E or log(pi*E), 625 x n
   double* loglik;               // [nblocks]                       (MODE_FWD_LL)
-  double* alpha;                // [total x XR] rescaled forward rows (FWD_STORE out, BWD in)
+  double* alpha;                // [total x XR] rescaled forward rows (FWD_STORE out, BWD in);
+                                //   Viterbi: the omega rows (MODE_VIT out)
   double* post;                 // [total x n] posteriors          (MODE_BWD)
   double* sink;                 // [64] write target of padded states (MODE_BWD)
-  uint8_t* bp;                  // [total x XR] back-pointers      (MODE_VIT)
-  uint8_t* chunk_map;           // [nchunks x XR] chunk origin maps (MODE_VIT)
-  const int64_t* chunk_base;    // [nblocks] first chunk of each block
+  uint8_t* stay;                // [n x fs] 1 where bp(t, j) == j is certain (MODE_VIT)
+  int64_t fs;                   // row stride of `stay` (>= total)
   uint8_t* last_state;          // [nblocks] argmax of the last column (MODE_VIT)
   int prio_len;                 // blocks at least this long run at raised wave priority
   uint64_t* diag;               // diagnostic build only: per-segment cycle sums
@@ -49,10 +46,23 @@ SweepGeometry sweep_geometry(int n, int mode);
 int sweep_row_stride(int n, int mode);
 hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepArgs& a,
                         hipStream_t st);
-hipError_t launch_vit_traceback(int n, int64_t nblocks, int64_t nchunks, const int64_t* off,
-                                const int64_t* chunk_base, const int32_t* chunk_blk,
-                                const uint8_t* chunk_map, const uint8_t* last_state,
-                                uint8_t* chunk_end, const uint8_t* bp, uint8_t* path,
-                                hipStream_t st);
+// Viterbi traceback over the omega rows and stay flags written by MODE_VIT
+struct TraceArgs {
+  int n;                      // hidden states
+  int xr;                     // row stride of the omega rows
+  int64_t fs;                 // row stride of the stay flags
+  int64_t nblocks;
+  const int64_t* off;         // [nblocks+1]
+  const int32_t* order;       // [nblocks] longest first
+  int* queue;                 // work counter, zero at launch
+  const uint16_t* obs;        // [total]
+  const double* log_a;        // n x n
+  const double* log_e;        // 625 x n
+  const double* omega;        // [total x xr]
+  const uint8_t* stay;        // [n x fs]
+  const uint8_t* last_state;  // [nblocks]
+  uint8_t* path;              // [total]
+};
+hipError_t launch_vit_traceback(const TraceArgs& a, int grid, hipStream_t st);
 
 }  // namespace itr
