@@ -56,6 +56,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="repeat the CPU-baseline sample until this much time has passed")
     ap.add_argument("--check", action="store_true", help="verify against the CPU oracle")
+    ap.add_argument("--concurrent", type=int, default=1,
+                    help="1: forward sweep on a side stream beside the Viterbi sweep")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the exchange with several ranks on one GPU)")
@@ -112,6 +114,10 @@ def main():
         d_ll_global = torch.zeros(nblk_global, dtype=torch.float64, device=cdev)
 
     fwd_ms, vit_ms, tb_ms = [], [], []
+    # forward log-likelihood and Viterbi are independent sweeps over the same resident
+    # columns: the forward runs on a side stream beside the Viterbi sweep, so the two
+    # kernels share the CUs and the long blocks of one overlap the bulk of the other
+    side = torch.cuda.Stream(device=dev) if args.concurrent else None
 
     def step(timing=False):
         if post_mode:
@@ -121,7 +127,15 @@ def main():
                 vit_ms.append(hmm.last_kernel_ms("posterior_bwd"))
                 tb_ms.append(0.0)
             return
-        hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
+        cur = torch.cuda.current_stream(dev)
+        if side is not None and not timing:
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
+            hmm.viterbi_device(model, plan, d_obs, out=d_path)
+            cur.wait_stream(side)
+        else:
+            hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
         if timing:
             fwd_ms.append(hmm.last_kernel_ms("forward"))
         if world > 1:
@@ -130,7 +144,8 @@ def main():
             d_ll_global.zero_()
             d_ll_global[first:first + plan.nblocks] = d_ll.to(cdev)
             dist.all_reduce(d_ll_global)
-        hmm.viterbi_device(model, plan, d_obs, out=d_path)
+        if side is None or timing:
+            hmm.viterbi_device(model, plan, d_obs, out=d_path)
         if timing:
             vit_ms.append(hmm.last_kernel_ms("viterbi"))
             tb_ms.append(hmm.last_kernel_ms("traceback"))

@@ -118,7 +118,7 @@ struct itr_plan {
   int64_t nblocks = 0, total = 0;
   int64_t* d_off = nullptr;
   int32_t* d_order = nullptr;
-  int* d_queue = nullptr;  // [0] sweep work counter, [1] traceback work counter
+  int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
   // workspace (grown on demand): forward rows (posterior) or omega rows (Viterbi), and the
@@ -382,6 +382,7 @@ int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
   a.mat = m->la;
   a.emit = m->LE;
   a.init = m->LPIE;
+  a.queue = p->d_queue + 2;  // own counter: may run concurrently with a forward sweep
   a.alpha = p->d_alpha;
   a.stay = p->d_stay;
   a.fs = stay_stride(p->total);
