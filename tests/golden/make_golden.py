@@ -19,6 +19,9 @@ Fixtures are DATA only (inputs + expected outputs), written as .npz:
                         reference's forward_loglik / viterbi+backtrack_viterbi / post_prob
                         outputs (optimizer.py:145-354)
   expm_kat.npz          reference expm (expm.py:9-167) on matrices hitting every Pade branch
+  derive_times.json     the arguments optimization_wrapper (optimizer.py:396-557) passes to
+                        trans_emiss_calc for every time-parameter case, captured by
+                        replacing trans_emiss_calc in the imported reference module
 
 Usage:  python tests/golden/make_golden.py alphabet|sweeps|expm|model <tag> ...
 """
@@ -255,6 +258,55 @@ def cmd_expm():
     print("expm_kat.npz written")
 
 
+class _Captured(Exception):
+    pass
+
+
+def cmd_derive():
+    """Every case of optimizer.py:419-541, t_out derived and fixed, two ABC interval
+    counts; the reference's optimization_wrapper runs until it calls trans_emiss_calc."""
+    import json
+    import tempfile
+
+    _import_reference()
+    import itrails.optimizer as ref_opt
+
+    def capture(*args):
+        raise _Captured(args)
+
+    ref_opt.trans_emiss_calc = capture
+    mu = 2e-8
+    base = dict(t_1=240000.0, t_A=250000.0, t_B=230000.0, t_C=290000.0, t_2=40000.0,
+                t_upper=745069.3855, N_AB=30000.0, N_ABC=50000.0, r=1e-8, t_out=2.5e6)
+    cases = [["t_A", "t_B", "t_C"], ["t_1", "t_A"], ["t_1", "t_B"], ["t_1", "t_C"],
+             ["t_A", "t_B"], ["t_A", "t_C"], ["t_B", "t_C"], ["t_1"]]
+    out = []
+    tmp = tempfile.mkdtemp()
+    for case in cases:
+        for fixed_out in (False, True):
+            for n_abc in (3, 5):
+                # optimized: the case's times + N_ABC + t_upper; fixed: the rest (mu-scaled)
+                names = list(case) + ["N_ABC", "t_upper"]
+                d = {"n_int_AB": 3, "n_int_ABC": n_abc, "t_2": base["t_2"] * mu,
+                     "N_AB": base["N_AB"] * mu, "r": base["r"] / mu}
+                if fixed_out:
+                    d["t_out"] = base["t_out"] * mu
+                args = [base[k] * mu for k in names]
+                try:
+                    ref_opt.optimization_wrapper(np.array(args), names, frozenset(case), d,
+                                                 [], os.path.join(tmp, "x"),
+                                                 {"Nfeval": 0, "time": 0.0})
+                    raise RuntimeError("trans_emiss_calc was not reached")
+                except _Captured as c:
+                    got = list(c.args[0])
+                out.append({"case": case, "names": names, "args": args, "fixed": d,
+                            "trans_emiss_args": [g if not isinstance(g, np.ndarray) else g.tolist()
+                                                 for g in got]})
+    with open(os.path.join(HERE, "derive_times.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(f"derive_times.json written ({len(out)} cases)")
+
+
 if __name__ == "__main__":
     cmd = sys.argv[1]
     if cmd == "alphabet":
@@ -266,5 +318,7 @@ if __name__ == "__main__":
         cmd_sweeps(tuple(sys.argv[2:]))
     elif cmd == "expm":
         cmd_expm()
+    elif cmd == "derive":
+        cmd_derive()
     else:
         raise SystemExit(__doc__)
