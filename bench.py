@@ -29,11 +29,25 @@ sys.path.insert(0, ROOT)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 (vector = matrix rate), AMD spec
 
 
+# KAT parameters, internal units of the {t_1} case: times and N times mu,
+# r over mu (workflow_optimize.py:360-380)
+MU = 2e-8
+KAT = {"t_1": 240000.0 * MU, "t_2": 40000.0 * MU, "N_AB": 50000.0 * MU, "N_ABC": 50000.0 * MU,
+       "t_upper": 745069.3855 * MU, "r": 1e-8 / MU}
+
+
 def load_model(n_int: int):
     f = os.path.join(ROOT, "tests", "golden", f"model_kat_{n_int}_{n_int}.npz")
     if os.path.exists(f):
         g = np.load(f)
         return g["a"], g["b"], g["pi"], f"itrails ({n_int},{n_int}) KAT model"
+    # (7,7): the reference build does not finish here; this is the device
+    # model build's output for the KAT parameters (scripts/model_timing.py)
+    f = os.path.join(ROOT, "tests", "data", f"model_device_{n_int}_{n_int}.npz")
+    if os.path.exists(f):
+        g = np.load(f)
+        return g["a"], g["b"], g["pi"], (f"itrails ({n_int},{n_int}) KAT model, built by the "
+                                         "device model build")
     # same state count, random HMM (only until the reference model fixture exists)
     n = {5: 70, 7: 133}.get(n_int, 70)
     g = np.load(os.path.join(ROOT, "tests", "golden", f"sweep_syn{n}.npz"))
@@ -46,9 +60,11 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n-int", type=int, default=5)
-    ap.add_argument("--mode", choices=["fv", "posterior"], default="fv",
+    ap.add_argument("--mode", choices=["fv", "posterior", "optimize"], default="fv",
                     help="fv: forward + Viterbi (BASELINE config 2, the default); posterior: "
-                         "posterior decoding (config 3)")
+                         "posterior decoding (config 3, use --n-int 7); optimize: one "
+                         "itrails-optimize objective evaluation per step = device model "
+                         "rebuild + forward log-likelihood of the resident columns (config 5)")
     ap.add_argument("--mbp", type=float, default=10.0, help="columns per GPU (Mbp)")
     ap.add_argument("--mean-block", type=float, default=2000.0)
     ap.add_argument("--cpu-sample", type=int, default=10_000_000,
@@ -98,6 +114,7 @@ def main():
     model = hmm.Model(a, b, pi)
     plan = hmm.Plan(off)
     post_mode = args.mode == "posterior"
+    opt_mode = args.mode == "optimize"
     plan.reserve(n, posterior=post_mode)
     d_obs = torch.from_numpy(obs.astype(np.int16)).to(dev)
     d_ll = torch.empty(plan.nblocks, dtype=torch.float64, device=dev)
@@ -119,7 +136,44 @@ def main():
     # kernels share the CUs and the long blocks of one overlap the bulk of the other
     side = torch.cuda.Stream(device=dev) if args.concurrent else None
 
+    build_ms = []
+    eval_no = [0]
+
+    def opt_step(timing=False):
+        # one objective evaluation at a nearby parameter vector (the simplex moves every
+        # call): model rebuild on the device, forward log-likelihood of every block,
+        # all-reduce of the per-block values (N > 1), host sum in block order
+        from itrails_amd.optimizer import model_for
+
+        eval_no[0] += 1
+        names = list(KAT)
+        x = [KAT[k] * (1.0 + 1e-3 * ((eval_no[0] + i) % 5 - 2)) for i, k in enumerate(names)]
+        tb = time.perf_counter()
+        _, (a1, b1, p1, _, _) = model_for(x, names, frozenset(["t_1"]),
+                                          {"n_int_AB": args.n_int, "n_int_ABC": args.n_int})
+        m1 = hmm.Model(a1, b1, p1)
+        build_ms.append((time.perf_counter() - tb) * 1e3)
+        hmm.forward_loglik_device(m1, plan, d_obs, out=d_ll)
+        if timing:
+            fwd_ms.append(hmm.last_kernel_ms("forward"))
+            vit_ms.append(hmm.last_kernel_ms("forward"))
+            tb_ms.append(0.0)
+        v = d_ll
+        if world > 1:
+            d_ll_global.zero_()
+            d_ll_global[first:first + plan.nblocks] = d_ll.to(cdev)
+            dist.all_reduce(d_ll_global)
+            v = d_ll_global
+        acc = 0.0
+        for y in v.cpu().numpy().tolist():
+            acc += y
+        m1.close()
+        return acc
+
     def step(timing=False):
+        if opt_mode:
+            opt_step(timing)
+            return
         if post_mode:
             hmm.posterior_device(model, plan, d_obs, out=d_post)
             if timing:
@@ -188,20 +242,32 @@ def main():
         # Viterbi: one add + one max per (i, j) pair; backward: one FMA
         ops_per_col = 2.0 * n * n
         achieved = ops_per_col * cols / (vit_avg * 1e-3) / 1e12
-        traffic, traffic_note = pmc_traffic(n, 2 if post_mode else 3)
+        traffic, traffic_note = pmc_traffic(n, {"fv": 3, "posterior": 2, "optimize": 0}[args.mode])
         cpu = None
-        if args.cpu_sample > 0:
+        if opt_mode:
+            # the reference's own model build: 615 s per (5,5) evaluation on the 8-core
+            # survey container; it cannot run on the GPU box
+            cpu = {"value": round(1.0 / 615.0, 6), "unit": "evaluations/s", "cores": 8,
+                   "kind": "reference",
+                   "sample": "trans_emiss_calc (5,5) measured once in the build container "
+                             "(BASELINE.md 2), not re-timed on the GPU box"}
+        elif args.cpu_sample > 0:
             cpu = cpu_baseline(a, b, pi, obs, off, args.cpu_sample, args.cpu_seconds,
                                post_mode)
         check = None
-        if args.check and not post_mode:
+        if args.check and args.mode == "fv":
             check = verify(a, b, pi, obs, off, ll_host if world == 1 else d_ll.cpu().numpy(),
                            d_path.cpu().numpy())
+        metric = {"fv": "alignment columns/s (forward+Viterbi), 3sp+outgroup HMM",
+                  "posterior": "alignment columns/s (posterior decoding), 3sp+outgroup HMM",
+                  "optimize": "itrails-optimize objective evaluations/s (device model rebuild "
+                              "+ forward loglik of the resident alignment)"}[args.mode]
+        if opt_mode:
+            value = args.steps / dt
         result = {
-            "metric": ("alignment columns/s (posterior decoding), 3sp+outgroup HMM" if post_mode
-                       else "alignment columns/s (forward+Viterbi), 3sp+outgroup HMM"),
-            "value": round(value, 1),
-            "unit": "columns/s",
+            "metric": metric,
+            "value": round(value, 4 if opt_mode else 1),
+            "unit": "evaluations/s" if opt_mode else "columns/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -210,17 +276,20 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: columns sampled from the reference's (5,5) KAT model, "
+            "data": f"synthetic: columns sampled from the {model_name}, "
                     "geometric blocks mean 2 kbp, 1% gaps + 0.5% N",
             "config": {"workload": f"{args.mbp:g} Mbp/GPU, {n_int_label(args.n_int)}, " +
-                                   ("posterior decoding" if post_mode else
-                                    "forward loglik + Viterbi traceback"),
+                                   {"fv": "forward loglik + Viterbi traceback",
+                                    "posterior": "posterior decoding",
+                                    "optimize": "model rebuild + forward loglik per "
+                                                "evaluation"}[args.mode],
                        "model": model_name, "hidden_states": n,
                        "columns_per_gpu": cols, "blocks_per_gpu": int(plan.nblocks),
                        "longest_block": int(np.diff(off).max()),
                        "parallelism": f"block-sharded x{world}"},
-            "roofline": {"kernel": ("sweep_kernel<BWD> (backward + posterior)" if post_mode
-                                    else "sweep_kernel<VIT> (Viterbi max-plus)"),
+            "roofline": {"kernel": {"fv": "sweep_kernel<VIT> (Viterbi max-plus)",
+                                    "posterior": "sweep_kernel<BWD> (backward + posterior)",
+                                    "optimize": "sweep_kernel<FWD_LL> (forward)"}[args.mode],
                          "bound": "mfma", "pipe": "FP64 VALU (add/max; FP64 vector rate = "
                                                   "FP64 matrix rate on MI355X)",
                          "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
@@ -232,6 +301,7 @@ def main():
                          "traceback_ms": round(float(np.mean(tb_ms)), 4),
                          "algorithmic": f"{ops_per_col:.0f} FP64 ops/column x {cols} columns"},
             "cpu_baseline": cpu,
+            **({"build_ms": round(float(np.mean(build_ms)), 1)} if opt_mode else {}),
             "loglik_total": ll_total,
             "gen_seconds": round(gen_s, 2),
         }
