@@ -72,7 +72,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="repeat the CPU-baseline sample until this much time has passed")
     ap.add_argument("--check", action="store_true", help="verify against the CPU oracle")
-    ap.add_argument("--concurrent", type=int, default=1,
+    ap.add_argument("--concurrent", type=int, default=0,
                     help="1: forward sweep on a side stream beside the Viterbi sweep")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
@@ -330,8 +330,8 @@ def pmc_traffic(n, mode=3):
                     and v.get("n_states", 70) == n and "hbm_bytes_raw" in v:
                 return round(v["hbm_bytes_raw"]), (
                     f"{os.path.basename(f)} ({name}): FETCH_SIZE+WRITE_SIZE per launch, raw; "
-                    "Viterbi writes are the uint8 back-pointer rows (padded-state stride), "
-                    "posterior writes the f64 rows")
+                    "the Viterbi sweep writes the f64 omega rows (padded-state stride) and "
+                    "the uint8 stay flags, the posterior sweep the f64 posterior rows")
     return None, "no PMC summary under profiles/"
 
 

@@ -121,6 +121,7 @@ struct itr_plan {
   int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
+  std::vector<int64_t> sorted_len;  // block lengths, longest first (processing order)
   // workspace (grown on demand): forward rows (posterior) or omega rows (Viterbi), and the
   // Viterbi stay flags
   uint8_t* d_stay = nullptr;
@@ -304,6 +305,8 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
     return h_off[x + 1] - h_off[x] > h_off[y + 1] - h_off[y];
   });
+  p->sorted_len.resize(nblocks);
+  for (int64_t k = 0; k < nblocks; ++k) p->sorted_len[k] = h_off[order[k] + 1] - h_off[order[k]];
   if (nblocks > 0) {
     const int64_t k = std::min<int64_t>(nblocks - 1, 255);
     const int64_t T = h_off[order[k] + 1] - h_off[order[k]];
@@ -312,7 +315,7 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   int e = 0;
   if (!e) e = dev_alloc(&p->d_off, nblocks + 1);
   if (!e) e = dev_alloc(&p->d_order, nblocks);
-  if (!e) e = dev_alloc(&p->d_queue, 4);
+  if (!e) e = dev_alloc(&p->d_queue, 8);
   if (!e) e = dev_alloc(&p->d_sink, 64);
   if (!e) e = dev_alloc(&p->d_last, nblocks);
   auto up = [&](void* d, const void* h, size_t bytes) {
@@ -387,7 +390,36 @@ int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
   a.stay = p->d_stay;
   a.fs = stay_stride(p->total);
   a.last_state = p->d_last;
-  if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
+  const itr::SweepGeometry pg = itr::pair_geometry(m->n);
+  if (pg.iq >= 0 && p->nblocks >= 2) {
+    // the longest blocks (at least half as long as the longest, at most one per CU) run
+    // one per workgroup; every other block is paired with its neighbour in the
+    // longest-first order
+    const char* fr = getenv("ITR_PAIR_SINGLE_FRAC");
+    const double frac = fr ? atof(fr) : 0.5;
+    int64_t ns = 0;
+    const int64_t longest = p->sorted_len[0];
+    while (ns < p->nblocks && ns < cu_count() &&
+           (double)p->sorted_len[ns] >= frac * (double)longest && longest > 0)
+      ++ns;
+    int64_t grid = (int64_t)pg.per_cu * cu_count();
+    const int64_t work = ns + (p->nblocks - ns + 1) / 2;
+    if (grid > work) grid = work;
+    itr::SweepArgs ps = a;  // single-block part: order[0, ns)
+    ps.nblocks = ns;
+    ps.queue = p->d_queue + 3;
+    ps.nsingle_wg = (int)std::min<int64_t>(ns, grid);
+    a.order = p->d_order + ns;
+    a.nblocks = p->nblocks - ns;
+    HIP_TRY(hipMemsetAsync(p->d_queue + 2, 0, 2 * sizeof(int), st));
+    if (getenv("ITR_VERBOSE"))
+      fprintf(stderr, "[itr] viterbi pairs: n=%d w=%d lds=%zu per_cu=%d grid=%lld singles=%lld\n",
+              m->n, pg.iq, pg.lds, pg.per_cu, (long long)grid, (long long)ns);
+    Scope sc("viterbi", st);
+    HIP_TRY(itr::launch_vit_pairs(pg, (int)grid, a, ps, st));
+  } else {
+    if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
+  }
   itr::TraceArgs ta{};
   ta.n = m->n;
   ta.xr = itr::sweep_row_stride(m->n, itr::MODE_VIT);

@@ -41,6 +41,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "sweeps.h"
 
 namespace itr {
@@ -261,8 +263,7 @@ struct Occ {
 };
 
 template <int QL, int WV, int RJN, int IQ, int MODE>
-__global__ void __launch_bounds__(64 * WV, (Occ<QL, WV, RJN, IQ, MODE>::value))
-    sweep_kernel(SweepArgs p) {
+__device__ __forceinline__ void sweep_device(const SweepArgs& p) {
   constexpr int W = WV;       // wavefronts per workgroup
   constexpr int TB = 64 * W;  // threads per workgroup
   constexpr int IQS = IQ + (IQ & 1);  // 16-byte aligned source ranges in LDS
@@ -719,6 +720,230 @@ __global__ void __launch_bounds__(64 * WV, (Occ<QL, WV, RJN, IQ, MODE>::value))
   DIAG_FLUSH();
 }
 
+template <int QL, int WV, int RJN, int IQ, int MODE>
+__global__ void __launch_bounds__(64 * WV, (Occ<QL, WV, RJN, IQ, MODE>::value))
+    sweep_kernel(SweepArgs p) {
+  sweep_device<QL, WV, RJN, IQ, MODE>(p);
+}
+
+// ---------------------------------------------------------------------------------------
+// Paired Viterbi sweep: two MAF blocks of similar length per workgroup (neighbours in the
+// longest-first order).  Both blocks use the same transition matrix, so every lane's IQ
+// slice of log a serves two max-plus chains (one per block) and the 8-lane combine becomes
+// a reduce-scatter: the first DPP stage (q <-> 7 - q) hands each lane the other block's
+// partial of its own "home" block (q < 4: the first block, q >= 4: the second), the two
+// quad stages finish the maximum, and everything after the combine — the diagonal /
+// emission tail, the stay flag, the omega row store, the next step's publish — runs once
+// per lane for one block instead of once per lane for every block.  Per column that is
+// about a quarter fewer VALU instructions than the single-block sweep.  The two blocks'
+// published vectors live in two LDS regions 256-B apart in bank phase, so the combined
+// read pattern is the single-block one.  Blocks shorter than the pair's longer one simply
+// stop storing; the longest blocks of the launch (p_single) run one per workgroup on the
+// single-block path first, because there the step latency, not the instruction count,
+// bounds the launch.
+// ---------------------------------------------------------------------------------------
+template <int WV, int IQ>
+struct PairLds {
+  static constexpr int IQS = IQ + (IQ & 1);
+  static constexpr int XS = 8 * IQS;
+  static constexpr int XP = ((XS + 64 + 31) / 32) * 32;  // region stride: a 256-B multiple
+  static constexpr int XR = WV * 8;
+  static constexpr int TE = 16;
+  static constexpr size_t bytes = (size_t)4 * XP * 8 + (size_t)2 * 2 * TE * XR * 8 +
+                                  (size_t)128 * 8 + 40 * 4 + (size_t)2 * 2 * 64 * WV * 2;
+};
+
+template <int WV, int IQ>
+__device__ __forceinline__ void vit_pair_device(const SweepArgs& p) {
+  using L = PairLds<WV, IQ>;
+  constexpr int W = WV;
+  constexpr int TB = 64 * W;
+  constexpr int IQS = L::IQS, XS = L::XS, XP = L::XP, XR = L::XR, TE = L::TE;
+  constexpr int NCH = IQ >= 4 ? 2 : 1;  // chains per block (two blocks interleave already)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = p.n;
+  const int tid = threadIdx.x;
+  const int w = uni(tid >> 6);
+  const int l = tid & 63;
+  const int q = l & 7;
+  const int jl = l >> 3;
+  const int hs = q >> 2;  // home position in the pair after the combine
+  const int j = w * 8 + jl;
+  const bool jv = j < n;
+
+  double* X = reinterpret_cast<double*>(smem);  // [2 pos][2 buf][XP]
+  double* EST = X + 4 * XP;                     // [2 pos][2][TE][XR]
+  double* RED = EST + 2 * 2 * TE * XR;          // [2 pos][64]
+  int* SBLK = reinterpret_cast<int*>(RED + 128);
+  int* REDI = SBLK + 8;                                     // [2 pos][16]
+  uint16_t* OBS = reinterpret_cast<uint16_t*>(REDI + 32);  // [2 pos][2][TB]
+
+  const bool pub = jv && (q & 3) == 0;
+  const int jx = pub ? (j / IQ) * IQS + j % IQ : XS + l;
+  double m[IQ];
+  const double ldiag = jv ? p.mat[(int64_t)j * n + j] : 0.0;
+#pragma unroll
+  for (int k = 0; k < IQ; ++k) {
+    const int i = q * IQ + k;
+    m[k] = (i < n && jv) ? p.mat[(int64_t)i * n + j] : 0.0;
+    if (i == j) m[k] = -INFINITY;
+  }
+  lds_barrier();  // the single-block phase may still be reading LDS
+  for (int i = tid; i < 4 * XP; i += TB) X[i] = -INFINITY;
+  lds_barrier();
+
+  RowStage<W, XR, TE> est0, est1;
+  const int npairs = (int)((p.nblocks + 1) / 2);
+  for (;;) {
+    if (tid == 0) SBLK[0] = atomicAdd(p.queue, 1);
+    lds_barrier();
+    const int pi = uni(SBLK[0]);
+    lds_barrier();
+    if (pi >= npairs) break;
+    const int b0 = uni(p.order[2 * pi]);
+    const bool has1 = 2 * pi + 1 < p.nblocks;
+    const int b1 = has1 ? uni(p.order[2 * pi + 1]) : b0;
+    const int64_t c00 = p.off[b0], c01 = p.off[b1];
+    const int T0 = uni((int)(p.off[b0 + 1] - c00));
+    const int T1 = has1 ? uni((int)(p.off[b1 + 1] - c01)) : 0;
+    const int T = max(T0, T1), Tmin = min(T0, T1);
+    if (T > 0) {
+      const int64_t ch = hs ? c01 : c00;  // this lane's home block
+      const int Th = hs ? T1 : T0;
+      ObsTiles ot0{OBS, p.obs + c00, T0, +1, TB, 0};
+      ObsTiles ot1{OBS + 2 * TB, p.obs + c01, T1, +1, TB, 0};
+      ot0.start(tid);
+      ot1.start(tid);
+      lds_barrier();
+      auto row0 = [&](int s) -> int64_t { return s < T0 ? (int64_t)ot0.get(s) : -1; };
+      auto row1 = [&](int s) -> int64_t { return s < T1 ? (int64_t)ot1.get(s) : -1; };
+      double* EST0 = EST;
+      double* EST1 = EST + 2 * TE * XR;
+      est0.issue(p.emit, n, n, tid, 0, row0);
+      est1.issue(p.emit, n, n, tid, 0, row1);
+      est0.commit(EST0, tid);
+      est1.commit(EST1, tid);
+      est0.issue(p.emit, n, n, tid, TE, row0);
+      est1.issue(p.emit, n, n, tid, TE, row1);
+      lds_barrier();
+      const double* ESTh = hs ? EST1 : EST0;
+      auto staged = [&](const double* base, int s) {
+        return base[((s / TE) & 1) * TE * XR + (s & (TE - 1)) * XR + j];
+      };
+      const int o0 = hs ? ot1.get(0) : ot0.get(0);
+      double x = (jv && Th > 0) ? p.init[o0 * n + j] : -INFINITY;
+      if (pub && Th > 0) p.alpha[ch * XR + j] = x;
+      uint8_t* srow = p.stay + (int64_t)j * p.fs + ch;
+      double xfin = x;  // the shorter block's last omega (column Tmin - 1)
+      wait_vmem_all();
+      for (int t0 = 0; t0 < T; t0 += TE) {
+#pragma unroll
+        for (int sub = 0; sub < TE; ++sub) {
+          const int t = t0 + sub;
+          if (t >= 1 && t < T) {
+            const int buf = sub & 1;  // t0 is even
+            double* Xh = X + (hs * 2 + buf) * XP;
+            const double* Xo = X + ((1 - hs) * 2 + buf) * XP;
+            Xh[jx] = x;
+            double ec = 0.0;
+            if (sub != 0) ec = staged(ESTh, t);
+            if (sub == 0) {
+              ot0.advance(t, tid);
+              ot1.advance(t, tid);
+              if (t >= TE) {
+                const int slot = (t / TE) & 1;
+                est0.commit(EST0 + slot * TE * XR, tid);
+                est1.commit(EST1 + slot * TE * XR, tid);
+              }
+            }
+            lds_barrier();
+            if (sub == 0) {
+              if (t >= TE) {
+                est0.issue(p.emit, n, n, tid, t + TE, row0);
+                est1.issue(p.emit, n, n, tid, t + TE, row1);
+              }
+              ec = staged(ESTh, t);
+            }
+            const double* xh = Xh + q * IQS;
+            const double* xo = Xo + q * IQS;
+            double bh[NCH], bo[NCH];
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+              bh[c] = xh[c] + m[c];
+              bo[c] = xo[c] + m[c];
+            }
+#pragma unroll
+            for (int k = NCH; k < IQ; ++k) {
+              bh[k % NCH] = fmax(bh[k % NCH], xh[k] + m[k]);
+              bo[k % NCH] = fmax(bo[k % NCH], xo[k] + m[k]);
+            }
+            double zh = bh[0], zo = bo[0];
+#pragma unroll
+            for (int c = 1; c < NCH; ++c) {
+              zh = fmax(zh, bh[c]);
+              zo = fmax(zo, bo[c]);
+            }
+            // reduce-scatter: lane q takes lane 7-q's partial of q's home block (which is
+            // 7-q's other block), then the two quad stages
+            zh = fmax(zh, dpp_f64<DPP_HM>(zo));
+            zh = fmax(zh, dpp_f64<DPP_Q1>(zh));
+            zh = fmax(zh, dpp_f64<DPP_Q2>(zh));
+            const double yd = (x + ldiag) + ec;
+            const double yo = zh + ec;
+            const bool st = yd > yo;
+            x = fmax(yd, yo);
+            if (pub && t < Th) {
+              p.alpha[(ch + t) * XR + j] = x;
+              srow[t] = (uint8_t)st;
+            }
+            if (t == Tmin - 1) xfin = x;
+          }
+        }
+      }
+      // last state of each block = first argmax of its last omega row (optimizer.py:346)
+#pragma unroll
+      for (int pos = 0; pos < 2; ++pos) {
+        const int Tp = pos ? T1 : T0;
+        double bv = (hs == pos && jv && Tp > 0) ? (Tp == T ? x : xfin) : -INFINITY;
+        int bj = (hs == pos && jv) ? j : 0x7fffffff;
+        wave_first_max(bv, bj);
+        if (l == 0) {
+          RED[pos * 64 + w] = bv;
+          REDI[pos * 16 + w] = bj;
+        }
+      }
+      lds_barrier();
+      if (tid < 2) {
+        const int pos = tid;
+        const int Tp = pos ? T1 : T0;
+        if (Tp > 0) {
+          double b = RED[pos * 64];
+          int a = REDI[pos * 16];
+          for (int v = 1; v < W; ++v) {
+            const double c = RED[pos * 64 + v];
+            const int ci = REDI[pos * 16 + v];
+            if (c > b || (c == b && ci < a)) {
+              b = c;
+              a = ci;
+            }
+          }
+          p.last_state[pos ? b1 : b0] = (uint8_t)a;
+        }
+      }
+    }
+    lds_barrier();
+  }
+}
+
+// the launch: workgroups [0, ps.nsingle_wg) first run the longest blocks one at a time,
+// then every workgroup works through the pairs
+template <int WV, int IQ>
+__global__ void __launch_bounds__(64 * WV, (Occ<8, WV, 1, IQ, MODE_VIT>::value))
+    vit_pair_kernel(SweepArgs p, SweepArgs ps) {
+  if ((int)blockIdx.x < ps.nsingle_wg) sweep_device<8, WV, 1, IQ, MODE_VIT>(ps);
+  vit_pair_device<WV, IQ>(p);
+}
+
 // ---------------------------------------------------------------------------------------
 // Viterbi traceback (optimizer.py:336-354) over the omega rows and stay flags of MODE_VIT.
 // One wave per block (longest first from a work counter).  Walking down from the last
@@ -933,6 +1158,57 @@ hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepA
 int sweep_row_stride(int n, int mode) {  // padded target states: row stride of bp / alpha
   const int c = pick_cfg(n, mode);
   return c < 0 ? -1 : cfg_xr(c);
+}
+
+// Paired Viterbi sweep configurations: (waves, sources per lane) by state count
+// Opt-in (ITR_VIT_PAIRS=1): measured on the (5,5) model the paired sweep needs 13 % fewer
+// VALU instructions per column but its step takes 1.8x as long, so at two workgroups per CU
+// it is 5 % slower than the single-block sweep.
+static int pair_cfg(int n) {
+  if (!getenv("ITR_VIT_PAIRS")) return -1;
+  if (n > 64 && n <= 72) return 9;
+  if (n > 32 && n <= 64) return 8;
+  if (n > 16 && n <= 32) return 4;
+  return -1;
+}
+
+SweepGeometry pair_geometry(int n) {
+  SweepGeometry g{};
+  g.iq = pair_cfg(n);
+  if (g.iq < 0) return g;
+  const int w = g.iq;
+  g.block = 64 * w;
+  const int single_cfg = w == 9 ? 9 : (w == 8 ? 8 : 7);
+  size_t pl = 0;
+  int occ = 0;
+  switch (w) {
+    case 9: pl = PairLds<9, 9>::bytes; break;
+    case 8: pl = PairLds<8, 8>::bytes; break;
+    case 4: pl = PairLds<4, 4>::bytes; break;
+  }
+  g.lds = std::max(pl, lds_bytes(single_cfg, MODE_VIT));
+  hipError_t e = hipSuccess;
+  switch (w) {
+    case 9: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vit_pair_kernel<9, 9>, 576, g.lds); break;
+    case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vit_pair_kernel<8, 8>, 512, g.lds); break;
+    case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vit_pair_kernel<4, 4>, 256, g.lds); break;
+  }
+  g.per_cu = (e == hipSuccess && occ > 0) ? occ : 1;
+  const char* pcu = getenv("ITR_PAIR_PER_CU");
+  if (pcu && atoi(pcu) > 0) g.per_cu = atoi(pcu);
+  g.xp = single_cfg;  // the single-block configuration (row stride = its XR = 8 w)
+  return g;
+}
+
+hipError_t launch_vit_pairs(const SweepGeometry& g, int grid, const SweepArgs& p,
+                            const SweepArgs& ps, hipStream_t st) {
+  switch (g.iq) {
+    case 9: hipLaunchKernelGGL((vit_pair_kernel<9, 9>), dim3(grid), dim3(576), g.lds, st, p, ps); break;
+    case 8: hipLaunchKernelGGL((vit_pair_kernel<8, 8>), dim3(grid), dim3(512), g.lds, st, p, ps); break;
+    case 4: hipLaunchKernelGGL((vit_pair_kernel<4, 4>), dim3(grid), dim3(256), g.lds, st, p, ps); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_vit_traceback(const TraceArgs& a, int grid, hipStream_t st) {

@@ -28,6 +28,8 @@ struct SweepArgs {
   int64_t fs;                   // row stride of `stay` (>= total)
   uint8_t* last_state;          // [nblocks] argmax of the last column (MODE_VIT)
   int prio_len;                 // blocks at least this long run at raised wave priority
+  int nsingle_wg;               // paired Viterbi launch: workgroups that first run the
+                                //   single-block sweep over the longest blocks
   uint64_t* diag;               // diagnostic build only: per-segment cycle sums
   int diag_wave;                // diagnostic build only: the wave that reports
 };
@@ -46,6 +48,12 @@ SweepGeometry sweep_geometry(int n, int mode);
 int sweep_row_stride(int n, int mode);
 hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepArgs& a,
                         hipStream_t st);
+// Paired Viterbi sweep (two blocks per workgroup; g.iq < 0: not available for this n)
+SweepGeometry pair_geometry(int n);
+// p: the paired blocks (order / nblocks of the pairs), ps: the single-block part
+hipError_t launch_vit_pairs(const SweepGeometry& g, int grid, const SweepArgs& p,
+                            const SweepArgs& ps, hipStream_t st);
+
 // Viterbi traceback over the omega rows and stay flags written by MODE_VIT
 struct TraceArgs {
   int n;                      // hidden states
