@@ -110,7 +110,7 @@ struct itr_model {
   int device = 0;
   int n = 0;
   double *a = nullptr, *la = nullptr, *E = nullptr, *LE = nullptr, *PIE = nullptr,
-         *LPIE = nullptr;
+         *LPIE = nullptr, *aT = nullptr;
 };
 
 struct itr_plan {
@@ -122,6 +122,12 @@ struct itr_plan {
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
   std::vector<int64_t> sorted_len;  // block lengths, longest first (processing order)
+  // forward log-likelihood tasks {block, split, slot} (split blocks: two halves) and the
+  // split blocks' scratch
+  int64_t ntasks = 0, nsplit = 0;
+  int32_t *d_tasks = nullptr, *d_split_blk = nullptr;
+  double* d_svec = nullptr;
+  int* d_sK = nullptr;
   // workspace (grown on demand): forward rows (posterior) or omega rows (Viterbi), and the
   // Viterbi stay flags
   uint8_t* d_stay = nullptr;
@@ -261,6 +267,17 @@ int itr_model_create(int n, const double* a, const double* la, const double* E,
       return e;
     }
   }
+  // a^T for the backward halves of split forward sweeps (a layout copy)
+  std::vector<double> at((size_t)n * n);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) at[(size_t)j * n + i] = a[(size_t)i * n + j];
+  int e = dev_alloc(&m->aT, nn);
+  if (!e && hipMemcpy(m->aT, at.data(), nn * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+    e = fail(ITR_EHIP, "table upload failed");
+  if (e) {
+    itr_model_destroy(m);
+    return e;
+  }
   *out = m;
   return 0;
 }
@@ -273,6 +290,7 @@ int itr_model_destroy(itr_model_t m) {
   dev_free(m->LE);
   dev_free(m->PIE);
   dev_free(m->LPIE);
+  dev_free(m->aT);
   delete m;
   return 0;
 }
@@ -312,7 +330,46 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
     const int64_t T = h_off[order[k] + 1] - h_off[order[k]];
     p->prio_len = (int)std::max<int64_t>(T, 1);
   }
+  // Forward log-likelihood tasks.  The longest block bounds the sweep's makespan (one
+  // workgroup steps it column by column), so blocks at least half as long as the longest
+  // (and >= 512 columns) become two half-length tasks — forward over the first half,
+  // textbook backward over the second — whose vectors fwd_split_combine_kernel joins.
+  // Tasks run longest first.
+  std::vector<int32_t> tasks, split_blk;
+  std::vector<int64_t> tlen;
+  {
+    const char* fr = getenv("ITR_SPLIT_FRAC");
+    const double frac = fr ? atof(fr) : 0.5;
+    const int64_t tmax = nblocks ? h_off[order[0] + 1] - h_off[order[0]] : 0;
+    for (int64_t k = 0; k < nblocks; ++k) {
+      const int32_t b = order[k];
+      const int64_t T = h_off[b + 1] - h_off[b];
+      if (frac > 0 && T >= 512 && (double)T >= frac * (double)tmax) {
+        const int32_t m = (int32_t)(T / 2), slot = (int32_t)split_blk.size();
+        split_blk.push_back(b);
+        tasks.insert(tasks.end(), {b, m, slot, b, -m, slot});
+        tlen.push_back(m);
+        tlen.push_back(T - m + 1);
+      } else {
+        tasks.insert(tasks.end(), {b, 0, 0});
+        tlen.push_back(T);
+      }
+    }
+    std::vector<int64_t> idx(tlen.size());
+    std::iota(idx.begin(), idx.end(), 0);
+    std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return tlen[x] > tlen[y]; });
+    std::vector<int32_t> sorted(tasks.size());
+    for (size_t k = 0; k < idx.size(); ++k)
+      for (int c = 0; c < 3; ++c) sorted[3 * k + c] = tasks[3 * idx[k] + c];
+    tasks.swap(sorted);
+  }
+  p->ntasks = (int64_t)tasks.size() / 3;
+  p->nsplit = (int64_t)split_blk.size();
   int e = 0;
+  if (!e) e = dev_alloc(&p->d_tasks, tasks.size());
+  if (!e) e = dev_alloc(&p->d_split_blk, split_blk.size());
+  if (!e) e = dev_alloc(&p->d_svec, (size_t)p->nsplit * 2 * 256);
+  if (!e) e = dev_alloc(&p->d_sK, (size_t)p->nsplit * 2);
   if (!e) e = dev_alloc(&p->d_off, nblocks + 1);
   if (!e) e = dev_alloc(&p->d_order, nblocks);
   if (!e) e = dev_alloc(&p->d_queue, 8);
@@ -325,6 +382,8 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   };
   up(p->d_off, h_off.data(), (nblocks + 1) * sizeof(int64_t));
   up(p->d_order, order.data(), nblocks * sizeof(int32_t));
+  up(p->d_tasks, tasks.data(), tasks.size() * sizeof(int32_t));
+  up(p->d_split_blk, split_blk.data(), split_blk.size() * sizeof(int32_t));
   if (e) {
     itr_plan_destroy(p);
     return e;
@@ -340,6 +399,10 @@ int itr_plan_destroy(itr_plan_t p) {
   dev_free(p->d_queue);
   dev_free(p->d_sink);
   dev_free(p->d_stay);
+  dev_free(p->d_tasks);
+  dev_free(p->d_split_blk);
+  dev_free(p->d_svec);
+  dev_free(p->d_sK);
   dev_free(p->d_last);
   dev_free(p->d_alpha);
   delete p;
@@ -367,10 +430,21 @@ int itr_forward_loglik(itr_model_t m, itr_plan_t p, const uint16_t* obs, double*
   hipStream_t st = (hipStream_t)stream;
   itr::SweepArgs a = base_args(m, p, obs);
   a.mat = m->a;
+  a.matT = m->aT;
   a.emit = m->E;
   a.init = m->PIE;
   a.loglik = loglik;
-  return run_sweep(itr::MODE_FWD_LL, a, st, "forward");
+  a.tasks = p->d_tasks;
+  a.nblocks = p->ntasks;
+  a.svec = p->d_svec;
+  a.sK = p->d_sK;
+  if (!a.tasks || (p->nsplit > 0 && (!a.svec || !a.sK || !p->d_split_blk)))
+    return fail(ITR_ESTATE, "forward task tables missing");
+  if (int e = run_sweep(itr::MODE_FWD_LL, a, st, "forward")) return e;
+  HIP_TRY(itr::launch_fwd_split_combine(m->n, itr::sweep_row_stride(m->n, itr::MODE_FWD_LL),
+                                        (int)p->nsplit, p->d_split_blk, p->d_svec, p->d_sK,
+                                        loglik, st));
+  return 0;
 }
 
 int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,

@@ -232,7 +232,8 @@ struct RowStage {
       const int idx = tid + e * TB;
       const int row = idx / XR, col = idx % XR;
       const int64_t src = row_of(s0 + row);
-      v[e] = (src >= 0 && col < ncol) ? g[src * stride + col] : 0.0;
+      // row -2: a row of ones (the backward half's last step, see the forward sweep)
+      v[e] = (src >= 0 && col < ncol) ? g[src * stride + col] : (src == -2 ? 1.0 : 0.0);
     }
   }
   __device__ __forceinline__ void commit(double* lds_tile, int tid) const {
@@ -315,7 +316,7 @@ __device__ __forceinline__ void sweep_device(const SweepArgs& p) {
   for (int r = 0; r < RJN; ++r)
     ldiag[r] = (MODE == MODE_VIT && jv[r]) ? p.mat[(int64_t)jr[r] * n + jr[r]] : 0.0;
 #pragma unroll
-  for (int k = 0; k < IQ; ++k) {
+  for (int k = 0; k < (MODE == MODE_FWD_LL ? 0 : IQ); ++k) {  // FWD_LL: loaded per task
     const int i = q * IQ + k;
 #pragma unroll
     for (int r = 0; r < RJN; ++r) {
@@ -341,9 +342,16 @@ __device__ __forceinline__ void sweep_device(const SweepArgs& p) {
     const int bi = uni(SBLK[0]);
     lds_barrier();
     if (bi >= p.nblocks) break;
-    const int blk = uni(p.order[bi]);
+    // forward log-likelihood tasks (itr_plan_create): {block, split, slot}; split 0 = the
+    // whole block, +m = columns [0, m) forward, -m = the backward half (see below)
+    const int32_t* td = (MODE == MODE_FWD_LL) ? p.tasks + 3 * bi : nullptr;
+    const int blk = uni(td ? td[0] : p.order[bi]);
+    const int split = td ? uni(td[1]) : 0;
+    const int slot = td ? uni(td[2]) : 0;
     const int64_t c0 = p.off[blk];
-    const int T = uni((int)(p.off[blk + 1] - c0));
+    const int Tb = uni((int)(p.off[blk + 1] - c0));
+    // steps + 1 of this task: the backward half runs Tb - m steps
+    const int T = split > 0 ? split : (split < 0 ? Tb + split + 1 : Tb);
     // NOTE: no `continue` in this loop.  With a barrier in the body, hipcc (ROCm 7.2)
     // structurizes a `continue` back to the head's `if (tid == 0)` as a lane-divergent
     // inner loop around the barrier, which deadlocks the workgroup.
@@ -352,10 +360,26 @@ __device__ __forceinline__ void sweep_device(const SweepArgs& p) {
     } else {
       const bool urgent = T >= p.prio_len;
       if (urgent) __builtin_amdgcn_s_setprio(2);
-      ObsTiles ot{OBS, p.obs + c0, T, (MODE == MODE_BWD) ? -1 : +1, TB, 0};
+      if constexpr (MODE == MODE_FWD_LL) {
+        // the slice of a, or of a^T for a backward half, loaded for every task (a few L2
+        // loads against thousands of steps; an unconditional load keeps m out of the
+        // loop-carried state)
+        const double* mp = split < 0 ? p.matT : p.mat;
+#pragma unroll
+        for (int k = 0; k < IQ; ++k) {
+          const int i = q * IQ + k;
+#pragma unroll
+          for (int r = 0; r < RJN; ++r)
+            m[k][r] = (i < n && jv[r]) ? mp[(int64_t)i * n + jr[r]] : 0.0;
+        }
+      }
+      ObsTiles ot{OBS, p.obs + c0, Tb, (MODE == MODE_BWD || split < 0) ? -1 : +1, TB, 0};
       ot.start(tid);
       lds_barrier();
-      auto sym_row = [&](int s) -> int64_t { return s < T ? (int64_t)ot.get(s) : -1; };
+      auto sym_row = [&](int s) -> int64_t {
+        if (split < 0) return s < T - 1 ? (int64_t)ot.get(s) : (s == T - 1 ? -2 : -1);
+        return s < T ? (int64_t)ot.get(s) : -1;
+      };
       auto fwd_row = [&](int s) -> int64_t { return s < T ? c0 + (T - 1 - s) : -1; };
       est.issue(p.emit, n, n, tid, 0, sym_row);
       est.commit(EST, tid);
@@ -389,10 +413,19 @@ __device__ __forceinline__ void sweep_device(const SweepArgs& p) {
         // ------------- forward: alpha_t = (alpha_{t-1} @ a) * e_t  (optimizer.py:181-187)
         // Rows written to p.alpha (posterior workspace) have stride XR: every lane stores,
         // padded states store 0, duplicates store the same value (no branches).
+        // Long blocks are split (meet in the middle, exact in real arithmetic):
+        //   log P = log sum_j alpha_{m-1}[j] beta_{m-1}[j],  beta_{Tb-1} = 1,
+        //   beta_{t-1} = a (e_t * beta_t)   (the textbook backward, not the reference's v @ a)
+        // The forward half runs columns [0, m).  The backward half carries
+        // x'_t = beta_t * e_t from x'_{Tb-1} = e_{Tb-1}: every step is "contract with a^T,
+        // multiply by the next column's emission" — the forward step's shape — and its last
+        // step multiplies by a row of ones, leaving beta_{m-1}.  Both halves run Tb/2 steps
+        // on different workgroups; fwd_split_combine_kernel forms the dot product.
         const int o0 = ot.get(0);
+        const double* x0tab = (MODE == MODE_FWD_LL && split < 0) ? p.emit : p.init;
         double x[RJN];
 #pragma unroll
-        for (int r = 0; r < RJN; ++r) x[r] = jv[r] ? p.init[o0 * n + jr[r]] : 0.0;
+        for (int r = 0; r < RJN; ++r) x[r] = jv[r] ? x0tab[o0 * n + jr[r]] : 0.0;
         if constexpr (MODE == MODE_FWD_STORE) {
 #pragma unroll
           for (int r = 0; r < RJN; ++r) p.alpha[c0 * XR + jr[r]] = x[r];
@@ -485,7 +518,16 @@ __device__ __forceinline__ void sweep_device(const SweepArgs& p) {
             }
           }
         }
-        if constexpr (MODE == MODE_FWD_LL) {
+        if (MODE == MODE_FWD_LL && split != 0) {
+          // half of a split block: the scaled vector and its exponent
+          const int side = split < 0;
+          if (q == 0) {
+#pragma unroll
+            for (int r = 0; r < RJN; ++r)
+              if (jv[r]) p.svec[((int64_t)slot * 2 + side) * XR + jr[r]] = x[r];
+          }
+          if (tid == 0) p.sK[slot * 2 + side] = K;
+        } else if constexpr (MODE == MODE_FWD_LL) {
           // log P = log(sum_j x_j) + K ln 2   (optimizer.py:160-162)
           double part = 0.0;
           if (q == 0) {
@@ -1208,6 +1250,29 @@ hipError_t launch_vit_pairs(const SweepGeometry& g, int grid, const SweepArgs& p
     case 4: hipLaunchKernelGGL((vit_pair_kernel<4, 4>), dim3(grid), dim3(256), g.lds, st, p, ps); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// log P of each split block from its two halves (one wave per block)
+__global__ void fwd_split_combine_kernel(int n, int xr, int nsplit, const int32_t* split_blk,
+                                         const double* svec, const int* sK, double* loglik) {
+  const int wv = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const int l = threadIdx.x & 63;
+  if (wv >= nsplit) return;
+  const double* a = svec + (int64_t)wv * 2 * xr;
+  const double* b = a + xr;
+  double part = 0.0;
+  for (int j = l; j < n; j += 64) part += a[j] * b[j];
+  part = wave_sum(part);
+  if (l == 0) loglik[split_blk[wv]] = log(part) + (double)(sK[2 * wv] + sK[2 * wv + 1]) * LN2;
+}
+
+hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,
+                                    const double* svec, const int* sK, double* loglik,
+                                    hipStream_t st) {
+  if (nsplit <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fwd_split_combine_kernel, dim3((nsplit + 3) / 4), dim3(256), 0, st, n, xr,
+                     nsplit, split_blk, svec, sK, loglik);
   return hipGetLastError();
 }
 

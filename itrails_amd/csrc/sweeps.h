@@ -17,6 +17,7 @@ struct SweepArgs {
   int* queue;                   // work counter, zero at launch
   const uint16_t* obs;          // [total] observed symbols
   const double* mat;            // a (forward/backward) or log a (Viterbi), n x n
+  const double* matT;           // a^T (MODE_FWD_LL: backward halves of split blocks)
   const double* emit;           // E or log E, 625 x n
   const double* init;           // pi*E or log(pi*E), 625 x n
   double* loglik;               // [nblocks]                       (MODE_FWD_LL)
@@ -28,6 +29,9 @@ struct SweepArgs {
   int64_t fs;                   // row stride of `stay` (>= total)
   uint8_t* last_state;          // [nblocks] argmax of the last column (MODE_VIT)
   int prio_len;                 // blocks at least this long run at raised wave priority
+  const int32_t* tasks;         // MODE_FWD_LL: [nblocks x 3] {block, split, slot}, see capi.cpp
+  double* svec;                 // MODE_FWD_LL: [nsplit x 2 x XR] vectors of split blocks
+  int* sK;                      // MODE_FWD_LL: [nsplit x 2] their power-of-two exponents
   int nsingle_wg;               // paired Viterbi launch: workgroups that first run the
                                 //   single-block sweep over the longest blocks
   uint64_t* diag;               // diagnostic build only: per-segment cycle sums
@@ -53,6 +57,11 @@ SweepGeometry pair_geometry(int n);
 // p: the paired blocks (order / nblocks of the pairs), ps: the single-block part
 hipError_t launch_vit_pairs(const SweepGeometry& g, int grid, const SweepArgs& p,
                             const SweepArgs& ps, hipStream_t st);
+
+// log-likelihoods of the split blocks of a forward sweep
+hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,
+                                    const double* svec, const int* sK, double* loglik,
+                                    hipStream_t st);
 
 // Viterbi traceback over the omega rows and stay flags written by MODE_VIT
 struct TraceArgs {
