@@ -25,7 +25,12 @@ def sweep_fixtures():
 
 
 def model_fixtures():
-    return sorted(os.path.basename(f) for f in glob.glob(os.path.join(GOLDEN, "model_*.npz")))
+    return sorted(os.path.basename(f) for f in glob.glob(os.path.join(GOLDEN, "model_*.npz"))
+                  if not os.path.basename(f).startswith("model_int_"))
+
+
+def int_model_fixtures():
+    return sorted(os.path.basename(f) for f in glob.glob(os.path.join(GOLDEN, "model_int_*.npz")))
 
 
 @pytest.fixture(scope="session")

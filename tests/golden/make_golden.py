@@ -22,8 +22,14 @@ Fixtures are DATA only (inputs + expected outputs), written as .npz:
   derive_times.json     the arguments optimization_wrapper (optimizer.py:396-557) passes to
                         trans_emiss_calc for every time-parameter case, captured by
                         replacing trans_emiss_calc in the imported reference module
+  model_int_<tag>.npz   a, b, pi, hidden state tuples from the introgression model build
+                        trans_emiss_calc_introgression (int_get_trans_emiss.py:9-185); ray
+                        (int_get_tab.py:5) is replaced by the standard library's process
+                        pool in tests/golden/_shim/ray
+  int_statespace.json   the CTMC state spaces and rate-symbol matrices load_trans_mat(1..3)
+                        returns (int_load_trans_mat.py:6-41), as sets of transitions
 
-Usage:  python tests/golden/make_golden.py alphabet|sweeps|expm|model <tag> ...
+Usage:  python tests/golden/make_golden.py alphabet|sweeps|expm|model|intmodel <tag> ...|intspace
 """
 import os
 import sys
@@ -128,6 +134,102 @@ def cmd_model(tag):
         n_int=np.array([n_ab, n_abc]), build_seconds=np.array(dt),
     )
     print(f"model_{tag}.npz written: N={a.shape[0]} in {dt:.1f}s")
+
+
+# --------------------------------------------------------------------------------------
+# introgression model (int_get_trans_emiss.py)
+# --------------------------------------------------------------------------------------
+INT_PARAMS = {
+    # the KAT set plus an introgression 20 kyr before the first speciation: {t_1} case of
+    # int_optimizer.py:504-520 (t_B = t_C = t_1 - t_m)
+    "ikat": dict(mu=2e-8, N_AB=50000.0, N_BC=40000.0, N_ABC=50000.0, t_1=240000.0,
+                 t_m=20000.0, t_2=40000.0, t_upper=745069.3855, r=1e-8, m=0.1),
+    # asymmetric: {t_A, t_B, t_C} case (int_optimizer.py:406-419), other Ne, more migration
+    "ialt": dict(mu=1.5e-8, N_AB=30000.0, N_BC=60000.0, N_ABC=70000.0, t_A=180000.0,
+                 t_B=150000.0, t_C=165000.0, t_m=25000.0, t_2=60000.0, t_upper=500000.0,
+                 r=2.5e-8, m=0.3),
+}
+INT_MODELS = {
+    "ikat_1_1": ("ikat", 1, 1), "ikat_2_2": ("ikat", 2, 2), "ikat_3_3": ("ikat", 3, 3),
+    "ialt_2_3": ("ialt", 2, 3), "ialt_3_2": ("ialt", 3, 2), "ikat_1_3": ("ikat", 1, 3),
+    "ikat_4_4": ("ikat", 4, 4),
+}
+INT_ARGS = ("t_A", "t_B", "t_C", "t_2", "t_upper", "t_out", "t_m", "N_AB", "N_BC", "N_ABC",
+            "r", "m")
+
+
+def int_scaled_args(pset, n_ab, n_abc):
+    """mu-scaled arguments of trans_emiss_calc_introgression, derived like
+    optimization_wrapper_introgression (int_optimizer.py:404-529)."""
+    from itrails.cutpoints import cutpoints_ABC
+
+    p = INT_PARAMS[pset]
+    mu = p["mu"]
+    d = {k: v * mu for k, v in p.items() if k not in ("mu", "r", "m")}
+    d["r"] = p["r"] / mu
+    d["m"] = p["m"]
+    cut_ABC = cutpoints_ABC(n_abc, 1)
+    if "t_1" in d:
+        d["t_A"] = d["t_1"]
+        d["t_B"] = d["t_C"] = d["t_1"] - d["t_m"]
+        d["t_out"] = (d["t_1"] + d["t_2"] + cut_ABC[n_abc - 1] * d["N_ABC"] + d["t_upper"]
+                      + 2 * d["N_ABC"])
+        d.pop("t_1")
+    else:
+        d["t_out"] = (((d["t_A"] + (d["t_B"] + d["t_m"])) / 2 + d["t_2"])
+                      + (d["t_C"] + d["t_m"] + d["t_2"]) / 2
+                      + cut_ABC[n_abc - 1] * d["N_ABC"] + d["t_upper"] + 2 * d["N_ABC"])
+    return d
+
+
+def cmd_intmodel(tag):
+    import tempfile
+
+    _import_reference()
+    from itrails.int_get_trans_emiss import trans_emiss_calc_introgression
+
+    pset, n_ab, n_abc = INT_MODELS[tag]
+    d = int_scaled_args(pset, n_ab, n_abc)
+    t0 = time.time()
+    a, b, pi, hidden, observed = trans_emiss_calc_introgression(
+        *[d[k] for k in INT_ARGS], n_ab, n_abc, "standard", "standard", tempfile.mkdtemp())
+    dt = time.time() - t0
+    hidden_arr = np.array([hidden[i] for i in range(len(hidden))], dtype=np.int64)
+    obs_names = np.array([observed[i] for i in range(len(observed))])
+    np.savez_compressed(
+        os.path.join(HERE, f"model_int_{tag}.npz"),
+        a=a, b=b, pi=pi, hidden=hidden_arr, observed=obs_names,
+        args=np.array([d[k] for k in INT_ARGS]), n_int=np.array([n_ab, n_abc]),
+        build_seconds=np.array(dt),
+    )
+    print(f"model_int_{tag}.npz written: N={a.shape[0]} in {dt:.1f}s")
+
+
+def cmd_intspace():
+    import json
+    from ast import literal_eval
+
+    _import_reference()
+    from itrails.int_load_trans_mat import load_trans_mat
+
+    out = {}
+    for n_seq in (1, 2, 3):
+        mat, names = load_trans_mat(n_seq)
+        states = [repr(literal_eval(s)) for s in names]
+        trans = sorted([states[i], states[j], str(mat[i, j])]
+                       for i in range(len(states)) for j in range(len(states))
+                       if str(mat[i, j]) != "0")
+        out[str(n_seq)] = {"absorbing_last_two": states[-2:], "first": states[:2],
+                           "n_states": len(states), "transitions": trans}
+    # the hand-written chain of one missing B lineage (int_get_joint_prob_mat.py:306-339)
+    from itrails.int_get_joint_prob_mat import load_trans_mat_miss
+
+    mat, names = load_trans_mat_miss()
+    out["miss"] = {"states": [repr(literal_eval(s)) for s in names],
+                   "symbols": [[str(v) for v in row] for row in mat]}
+    with open(os.path.join(HERE, "int_statespace.json"), "w") as f:
+        json.dump(out, f)
+    print("int_statespace.json written")
 
 
 # --------------------------------------------------------------------------------------
@@ -320,5 +422,10 @@ if __name__ == "__main__":
         cmd_expm()
     elif cmd == "derive":
         cmd_derive()
+    elif cmd == "intmodel":
+        for t in sys.argv[2:]:
+            cmd_intmodel(t)
+    elif cmd == "intspace":
+        cmd_intspace()
     else:
         raise SystemExit(__doc__)

@@ -9,7 +9,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import golden, model_fixtures, sweep_fixtures
+from conftest import golden, int_model_fixtures, model_fixtures, sweep_fixtures
 from itrails_amd import hmm
 from itrails_amd.synth import sample_alignment
 from itrails_amd.tables import build_tables
@@ -84,9 +84,12 @@ def test_ties_first_maximum(gpu):
     np.testing.assert_array_equal(hmm._paths(model, plan, obs), O.viterbi(t, obs, off))
 
 
-@pytest.mark.parametrize("name", [m for m in model_fixtures() if m != "model_kat_1_1.npz"])
+@pytest.mark.parametrize("name", [m for m in model_fixtures() if m != "model_kat_1_1.npz"]
+                         + int_model_fixtures())
 def test_reference_models_vs_oracle(gpu, name):
-    """The reference's own model builds (a, b, pi from trans_emiss_calc) on sampled data."""
+    """The reference's own model builds (a, b, pi from trans_emiss_calc and from
+    trans_emiss_calc_introgression, whose sweeps are the same functions,
+    int_optimizer.py:147-380) on sampled data."""
     g = golden(name)
     a, b, pi = g["a"], g["b"], g["pi"]
     rng = np.random.default_rng(3)
