@@ -3,6 +3,8 @@
   itrails-optimize  CONFIG.yaml [--input MAF] [--output DIR/PREFIX]       (workflow_optimize.py)
   itrails-viterbi   --config-file F --input MAF --output DIR/PREFIX [...]  (workflow_viterbi.py)
   itrails-posterior --config-file F --input MAF --output DIR/PREFIX [...]  (workflow_posterior.py)
+  itrails-int-optimize / itrails-int-viterbi / itrails-int-posterior: the same for the
+  introgression model (workflow_int_*.py; pyproject.toml:59-61)
 
 Same options, YAML keys, messages, errors and output files; the model build, the sweeps,
 the MAF reader and the CSV writers run on the device path / native library instead of
@@ -19,15 +21,17 @@ import yaml
 
 from . import __version__
 from .config import (apply_decode_overrides, load_config, resolve_decode,
-                     resolve_optimize)
+                     resolve_decode_int, resolve_optimize)
 
 
-def _decode_parser(kind: str) -> argparse.ArgumentParser:
-    """workflow_viterbi.py:21-86 (workflow_posterior.py: same options)."""
+def _decode_parser(kind: str, intro: bool = False) -> argparse.ArgumentParser:
+    """workflow_viterbi.py:21-86 (workflow_posterior.py: same options;
+    workflow_int_viterbi.py:23-92 adds --t_m, --N_BC and --m)."""
     label = "Viterbi" if kind == "viterbi" else "Posterior"
+    prog = f"itrails-int-{kind}" if intro else f"itrails-{kind}"
     p = argparse.ArgumentParser(
         description=f"Run {label} decoding using iTRAILS",
-        usage=f"itrails-{kind} --config-file CONFIG_FILE --input PATH_MAF --output OUTPUT_PATH "
+        usage=f"{prog} --config-file CONFIG_FILE --input PATH_MAF --output OUTPUT_PATH "
               "--PARAMETERS")
     p.add_argument("--version", action="version", version=f"%(prog)s {__version__}")
     p.add_argument("--config-file", type=str, required=False, help="Path to the YAML config file.")
@@ -45,6 +49,10 @@ def _decode_parser(kind: str) -> argparse.ArgumentParser:
                       ("--N_ABC", "Effective population size for ABC"),
                       ("--r", "Recombination rate")):
         p.add_argument(name, type=float, help=hlp)
+    if intro:
+        p.add_argument("--t_m", type=float, help="Time parameter t_m")
+        p.add_argument("--N_BC", type=float, help="Effective population size for BC")
+        p.add_argument("--m", type=float, help="Migration rate between species")
     p.add_argument("--n_cpu", type=int, help="Number of CPUs to use")
     p.add_argument("--species_list", nargs="+", help="List of species names")
     p.add_argument("--reference", type=str, help="Reference to polarize coordinates")
@@ -56,8 +64,8 @@ def _decode_parser(kind: str) -> argparse.ArgumentParser:
     return p
 
 
-def _setup_decode(kind: str, argv):
-    parser = _decode_parser(kind)
+def _setup_decode(kind: str, argv, intro: bool = False):
+    parser = _decode_parser(kind, intro)
     if not argv:
         parser.print_usage()
         sys.exit("Error: No arguments provided. Please provide either a config file, "
@@ -70,7 +78,8 @@ def _setup_decode(kind: str, argv):
             if config.get(key) is None:
                 config[key] = {}
     config = apply_decode_overrides(config, args)
-    return resolve_decode(config, args.input, args.output, kind=kind)
+    resolve = resolve_decode_int if intro else resolve_decode
+    return resolve(config, args.input, args.output, kind=kind)
 
 
 def _build_model(s):
@@ -83,6 +92,17 @@ def _build_model(s):
                             s.norm_cut_AB, s.norm_cut_ABC)
 
 
+def _build_model_int(s):
+    from .model.intro import trans_emiss_calc_introgression
+
+    d = s.params
+    print("Calculating transition and emission probability matrices.")
+    return trans_emiss_calc_introgression(
+        d["t_A"], d["t_B"], d["t_C"], d["t_2"], d["t_upper"], d["t_out"], d["t_m"], d["N_AB"],
+        d["N_BC"], d["N_ABC"], d["r"], d["m"], s.n_int_AB, s.n_int_ABC, s.norm_cut_AB,
+        s.norm_cut_ABC)
+
+
 def _read(s):
     from .maf import read_maf
 
@@ -91,28 +111,30 @@ def _read(s):
     return obs, off, coords
 
 
-def _hidden_states(s, hidden_names, posterior: bool):
-    from .writers import write_hidden_states_csv
+def _hidden_states(s, hidden_names, posterior: bool, intro: bool = False):
+    from .writers import write_hidden_states_csv, write_hidden_states_csv_int
 
     f = os.path.join(s.output_dir, f"{s.output_prefix}.hidden_states.csv")
     if os.path.exists(f):
         print(f"Warning: File '{f}' already exists.")
         f = os.path.join(s.output_dir, f"{s.output_prefix}.hidden_states_2.csv")
         print(f"Using an alternative file name: {f}")
-    write_hidden_states_csv(f, hidden_names, s.abs_cut_AB, s.abs_cut_ABC, posterior)
+    if intro:
+        write_hidden_states_csv_int(f, hidden_names, s.abs_cut_AB, s.abs_cut_ABC)
+    else:
+        write_hidden_states_csv(f, hidden_names, s.abs_cut_AB, s.abs_cut_ABC, posterior)
     print(f"Hidden states written to file {f}.")
 
 
-def viterbi_main(argv=None) -> None:
-    """itrails-viterbi (workflow_viterbi.py:19-745)."""
+def _viterbi(argv, intro: bool) -> None:
     from . import hmm
     from .writers import write_viterbi_csv
 
-    s = _setup_decode("viterbi", sys.argv[1:] if argv is None else argv)
+    s = _setup_decode("viterbi", sys.argv[1:] if argv is None else argv, intro)
     obs, off, coords = _read(s)
-    a, b, pi, hidden_names, _ = _build_model(s)
-    _hidden_states(s, hidden_names, posterior=False)
-    print("Running viterbi.")
+    a, b, pi, hidden_names, _ = (_build_model_int if intro else _build_model)(s)
+    _hidden_states(s, hidden_names, posterior=False, intro=intro)
+    print("Running viterbi decoding." if intro else "Running viterbi.")
     path = np.zeros(0, dtype=np.uint8)
     if off[-1]:
         model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
@@ -123,15 +145,14 @@ def viterbi_main(argv=None) -> None:
     print(f"Viterbi decoding complete. Results saved to {out}.")
 
 
-def posterior_main(argv=None) -> None:
-    """itrails-posterior (workflow_posterior.py:19-717)."""
+def _posterior(argv, intro: bool) -> None:
     from . import hmm
     from .writers import write_posterior_csv
 
-    s = _setup_decode("posterior", sys.argv[1:] if argv is None else argv)
+    s = _setup_decode("posterior", sys.argv[1:] if argv is None else argv, intro)
     obs, off, coords = _read(s)
-    a, b, pi, hidden_names, _ = _build_model(s)
-    _hidden_states(s, hidden_names, posterior=True)
+    a, b, pi, hidden_names, _ = (_build_model_int if intro else _build_model)(s)
+    _hidden_states(s, hidden_names, posterior=True, intro=intro)
     print("Running posterior decoding.")
     n = a.shape[0]
     post = np.zeros((0, n))
@@ -144,15 +165,36 @@ def posterior_main(argv=None) -> None:
     print(f"Posterior decoding complete. Results saved to {out}.")
 
 
-def optimize_main(argv=None) -> None:
-    """itrails-optimize (workflow_optimize.py:17-489)."""
+def viterbi_main(argv=None) -> None:
+    """itrails-viterbi (workflow_viterbi.py:19-745)."""
+    _viterbi(argv, intro=False)
+
+
+def posterior_main(argv=None) -> None:
+    """itrails-posterior (workflow_posterior.py:19-717)."""
+    _posterior(argv, intro=False)
+
+
+def int_viterbi_main(argv=None) -> None:
+    """itrails-int-viterbi (workflow_int_viterbi.py:21-776)."""
+    _viterbi(argv, intro=True)
+
+
+def int_posterior_main(argv=None) -> None:
+    """itrails-int-posterior (workflow_int_posterior.py:21-743)."""
+    _posterior(argv, intro=True)
+
+
+def _optimize(argv, intro: bool) -> None:
     from .maf import maf_parser
-    from .optimizer import optimizer
+    from .optimizer import optimizer, optimizer_introgression
 
     parser = argparse.ArgumentParser(
-        description="Optimize workflow using TRAILS",
-        usage="itrails-optimize <config.yaml> --output OUTPUT_PATH | itrails-optimize example "
-              "--output OUTPUT_PATH")
+        description=("Optimize workflow with introgression using TRAILS" if intro
+                     else "Optimize workflow using TRAILS"),
+        usage=("itrails-optimize <config.yaml> --input PATH_TO_MAF --output OUTPUT_PATH" if intro
+               else "itrails-optimize <config.yaml> --output OUTPUT_PATH | itrails-optimize "
+                    "example --output OUTPUT_PATH"))
     parser.add_argument("--version", action="version", version=f"%(prog)s {__version__}")
     parser.add_argument("config_file", type=str, help="Path to the YAML config file.")
     parser.add_argument("--input", type=str, required=False, help="Path to the MAF alignment file.")
@@ -160,27 +202,43 @@ def optimize_main(argv=None) -> None:
                         help="Path and prefix for output files to be stored. Format: 'directory/prefix'.")
     args = parser.parse_args(sys.argv[1:] if argv is None else argv)
     config = load_config(args.config_file)
-    s = resolve_optimize(config, args.input, args.output)
-    with open(os.path.join(s.output_dir, f"{s.output_prefix}.starting_params.yaml"), "w") as f:
+    s = resolve_optimize(config, args.input, args.output, intro=intro)
+    sep = "_" if intro else "."  # the introgression workflow names its files prefix_*.
+    with open(os.path.join(s.output_dir, f"{s.output_prefix}{sep}starting_params.yaml"), "w") as f:
         yaml.dump(s.starting_params, f, default_flow_style=False)
-    best = os.path.join(s.output_dir, f"{s.output_prefix}.best_model.yaml")
+    best = os.path.join(s.output_dir, f"{s.output_prefix}{sep}best_model.yaml")
     with open(best, "w") as f:
         yaml.dump(s.best_model, f)
     V_lst = maf_parser(s.maf_path, s.species_list)
     if V_lst is None:
         raise ValueError("Error reading MAF alignment file.")
     print("Running optimization...")
-    optimizer(optim_variables=s.optim_variables, optim_list=s.optim_list, bounds=s.bounds,
-              fixed_params=s.fixed, V_lst=V_lst, res_name=s.output, case=s.case,
-              method=s.method, header=True)
-    hist = os.path.join(s.output_dir, f"{s.output_prefix}.optimization_history.csv")
+    run = optimizer_introgression if intro else optimizer
+    run(optim_variables=s.optim_variables, optim_list=s.optim_list, bounds=s.bounds,
+        fixed_params=s.fixed, V_lst=V_lst, res_name=s.output, case=s.case,
+        method=s.method, header=True)
+    hist = os.path.join(s.output_dir, f"{s.output_prefix}{sep}optimization_history.csv")
     print(f"Optimization complete. Results saved to {hist}.\n Best model saved to {best}.")
 
 
+def optimize_main(argv=None) -> None:
+    """itrails-optimize (workflow_optimize.py:17-489)."""
+    _optimize(argv, intro=False)
+
+
+def int_optimize_main(argv=None) -> None:
+    """itrails-int-optimize (workflow_int_optimize.py:17-474)."""
+    _optimize(argv, intro=True)
+
+
 def main(argv=None) -> None:
-    """`python -m itrails_amd {optimize|viterbi|posterior} ...`"""
+    """`python -m itrails_amd {optimize|viterbi|posterior|int-optimize|int-viterbi|
+    int-posterior} ...`"""
     argv = sys.argv[1:] if argv is None else argv
-    cmds = {"optimize": optimize_main, "viterbi": viterbi_main, "posterior": posterior_main}
+    cmds = {"optimize": optimize_main, "viterbi": viterbi_main, "posterior": posterior_main,
+            "int-optimize": int_optimize_main, "int-viterbi": int_viterbi_main,
+            "int-posterior": int_posterior_main}
     if not argv or argv[0] not in cmds:
-        sys.exit("usage: python -m itrails_amd {optimize|viterbi|posterior} ...")
+        sys.exit("usage: python -m itrails_amd {optimize|viterbi|posterior|int-optimize|"
+                 "int-viterbi|int-posterior} ...")
     cmds[argv[0]](argv[1:])

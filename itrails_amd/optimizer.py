@@ -18,7 +18,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from . import hmm
-from .config import derive_times, update_best_model
+from .config import derive_times, derive_times_int, update_best_model
 from .model.emissions import cutpoints_ABC
 from .model.trans_emiss import trans_emiss_calc
 
@@ -132,4 +132,79 @@ def optimizer(optim_variables: List[str], optim_list: List[float], bounds, fixed
     return minimize(optimization_wrapper, x0=optim_list,
                     args=(optim_variables, case, dict(fixed_params), data, res_name,
                           {"Nfeval": 0, "time": time.time()}),
+                    method=method, bounds=bounds, options=opts)
+
+
+# ---------------------------------------------------------------------------------------
+# introgression model (int_optimizer.py:397-651)
+# ---------------------------------------------------------------------------------------
+
+
+def model_for_introgression(arg_lst, optimized_params: Sequence[str], case: frozenset, d: Dict,
+                            tmp_path: str = "./"):
+    """int_optimizer.py:404-548: the parameter dictionary of one evaluation and its HMM."""
+    from .model.intro import trans_emiss_calc_introgression
+
+    dd = dict(d)
+    for i, p in enumerate(optimized_params):
+        dd[p] = arg_lst[i]
+    last = cutpoints_ABC(dd["n_int_ABC"], 1)[dd["n_int_ABC"] - 1]
+    dd = derive_times_int(dd, case, last)
+    return dd, trans_emiss_calc_introgression(
+        dd["t_A"], dd["t_B"], dd["t_C"], dd["t_2"], dd["t_upper"], dd["t_out"], dd["t_m"],
+        dd["N_AB"], dd["N_BC"], dd["N_ABC"], dd["r"], dd["m"], dd["n_int_AB"],
+        dd["n_int_ABC"], "standard", "standard", tmp_path)
+
+
+def _write_state_tables(hidden_names: Dict, observed_names: Dict) -> None:
+    """int_optimizer.py:549-559: the first evaluation writes hidden_states.csv and
+    observed_states.csv into the working directory (pandas to_csv layout)."""
+    import csv
+
+    for name, col, table in (("hidden_states.csv", "hidden", hidden_names),
+                             ("observed_states.csv", "observed", observed_names)):
+        with open(name, "w", newline="") as f:
+            w = csv.writer(f, lineterminator="\n")
+            w.writerow(["idx", col])
+            for k, v in table.items():
+                w.writerow([k, v])
+
+
+def optimization_wrapper_introgression(arg_lst, optimized_params, case, d,
+                                       data: DeviceAlignment, res_name: str,
+                                       info: Dict) -> float:
+    """int_optimizer.py:397-586: one objective evaluation -> -loglik; history rows and the
+    best model go to {prefix}_optimization_history.csv / {prefix}_best_model.yaml."""
+    output_dir, output_prefix = os.path.split(res_name)
+    _, (a, b, pi, hidden, observed) = model_for_introgression(
+        arg_lst, optimized_params, case, d, info.get("tmp_path", "./"))
+    if info["Nfeval"] == 0 and _is_writer():
+        _write_state_tables(hidden, observed)
+    loglik = data.loglik(a, b, pi)
+    if _is_writer():
+        write_list([info["Nfeval"]] + list(np.asarray(arg_lst).tolist()) +
+                   [loglik, time.time() - info["time"]],
+                   os.path.join(output_dir, f"{output_prefix}_optimization_history.csv"))
+        update_best_model(os.path.join(output_dir, f"{output_prefix}_best_model.yaml"),
+                          optimized_params, arg_lst, loglik, info["Nfeval"])
+    info["Nfeval"] += 1
+    return -loglik
+
+
+def optimizer_introgression(optim_variables: List[str], optim_list: List[float], bounds,
+                            fixed_params: Dict, V_lst, res_name: str, case: frozenset,
+                            method: str = "Nelder-Mead", header: bool = True,
+                            tmp_path: str = "./", options: Optional[Dict] = None):
+    """int_optimizer.py:589-651 on the device path."""
+    from scipy.optimize import minimize
+
+    output_dir, output_prefix = os.path.split(res_name)
+    if header and _is_writer():
+        write_list(["n_eval"] + list(optim_variables) + ["loglik", "time"],
+                   os.path.join(output_dir, f"{output_prefix}_optimization_history.csv"))
+    data = V_lst if isinstance(V_lst, DeviceAlignment) else DeviceAlignment(V_lst)
+    opts = {"maxiter": 10000, "disp": True} if options is None else options
+    return minimize(optimization_wrapper_introgression, x0=optim_list,
+                    args=(optim_variables, case, dict(fixed_params), data, res_name,
+                          {"Nfeval": 0, "time": time.time(), "tmp_path": tmp_path}),
                     method=method, bounds=bounds, options=opts)

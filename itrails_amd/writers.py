@@ -13,6 +13,8 @@ from ._lib import check, lib
 
 TOPOLOGY = {0: "({sp1,sp2},sp3)", 1: "((sp1,sp2),sp3)", 2: "((sp1,sp3),sp2)",
             3: "((sp2,sp3),sp1)"}
+# the introgression CLIs add the introgressed V0 topology (workflow_int_viterbi.py:666-673)
+TOPOLOGY_INT = {**TOPOLOGY, 4: "({sp2,sp3},sp1)"}
 
 
 def _flat(blocks, dtype):
@@ -89,3 +91,22 @@ def write_hidden_states_csv(output_file: str, hidden_names: dict, abs_cut_AB: Se
             t1 = f"{cut1[sh[1]]:.2f}-{cut1[sh[1] + 1]:.2f}"
             t2 = f"{abs_cut_ABC[sh[2]]:.2f}-{abs_cut_ABC[sh[2] + 1]:.2f}"
             w.writerow([idx, TOPOLOGY.get(k, "Unknown"), t1, t2, sh])
+
+
+def write_hidden_states_csv_int(output_file: str, hidden_names: dict,
+                                abs_cut_AB: Sequence[float], abs_cut_ABC: Sequence[float]):
+    """hidden_states.csv of itrails-int-viterbi / itrails-int-posterior
+    (workflow_int_viterbi.py:666-712): written through pandas there, so '\\n' line ends;
+    the first-coalescent interval uses the AB cutpoints for topology 0 and the ABC
+    cutpoints for every other topology — the introgressed states (4, i, j) included,
+    although their i indexes a BC interval (kept as the reference labels it)."""
+    with open(output_file, "w", newline="") as f:
+        w = csv.writer(f, lineterminator="\n")
+        w.writerow(["state_idx", "topology", "interval_1st_coalescent",
+                    "interval_2nd_coalescent", "shorthand_name"])
+        for idx, sh in hidden_names.items():
+            k, i1, i2 = sh
+            cut1 = abs_cut_AB if k == 0 else abs_cut_ABC
+            t1 = f"{cut1[i1]:.2f}-{cut1[i1 + 1]:.2f}"
+            t2 = f"{abs_cut_ABC[i2]:.2f}-{abs_cut_ABC[i2 + 1]:.2f}"
+            w.writerow([idx, TOPOLOGY_INT.get(k, "Unknown"), t1, t2, sh])

@@ -26,6 +26,9 @@ Fixtures are DATA only (inputs + expected outputs), written as .npz:
                         trans_emiss_calc_introgression (int_get_trans_emiss.py:9-185); ray
                         (int_get_tab.py:5) is replaced by the standard library's process
                         pool in tests/golden/_shim/ray
+  int_derive_times.json the arguments optimization_wrapper_introgression
+                        (int_optimizer.py:397-548) passes to trans_emiss_calc_introgression
+                        for every time-parameter case (captured like derive_times.json)
   int_statespace.json   the CTMC state spaces and rate-symbol matrices load_trans_mat(1..3)
                         returns (int_load_trans_mat.py:6-41), as sets of transitions
 
@@ -409,6 +412,53 @@ def cmd_derive():
     print(f"derive_times.json written ({len(out)} cases)")
 
 
+def cmd_intderive():
+    """Every case of int_optimizer.py:404-529, t_out derived and fixed, two ABC interval
+    counts; the reference's wrapper runs until it calls trans_emiss_calc_introgression."""
+    import json
+    import tempfile
+
+    _import_reference()
+    import itrails.int_optimizer as ref_opt
+
+    def capture(*args):
+        raise _Captured(args)
+
+    ref_opt.trans_emiss_calc_introgression = capture
+    mu = 2e-8
+    base = dict(t_1=240000.0, t_A=250000.0, t_B=210000.0, t_C=230000.0, t_2=40000.0,
+                t_m=15000.0, t_upper=745069.3855, N_AB=30000.0, N_BC=45000.0, N_ABC=50000.0,
+                r=1e-8, m=0.2, t_out=2.5e6)
+    cases = [["t_A", "t_B", "t_C"], ["t_1", "t_A"], ["t_1", "t_B"], ["t_1", "t_C"],
+             ["t_A", "t_B"], ["t_A", "t_C"], ["t_B", "t_C"], ["t_1"]]
+    out = []
+    tmp = tempfile.mkdtemp()
+    for case in cases:
+        for fixed_out in (False, True):
+            for n_abc in (3, 5):
+                names = list(case) + ["N_ABC", "t_upper", "t_m", "m"]
+                d = {"n_int_AB": 3, "n_int_ABC": n_abc, "t_2": base["t_2"] * mu,
+                     "N_AB": base["N_AB"] * mu, "N_BC": base["N_BC"] * mu,
+                     "r": base["r"] / mu}
+                if fixed_out:
+                    d["t_out"] = base["t_out"] * mu
+                args = [base[k] * mu for k in names]
+                try:
+                    ref_opt.optimization_wrapper_introgression(
+                        np.array(args), names, frozenset(case), d, [],
+                        os.path.join(tmp, "x"),
+                        {"Nfeval": 1, "time": 0.0, "tmp_path": tmp})
+                    raise RuntimeError("trans_emiss_calc_introgression was not reached")
+                except _Captured as c:
+                    got = list(c.args[0])
+                out.append({"case": case, "names": names, "args": args, "fixed": d,
+                            "trans_emiss_args": [g if not isinstance(g, np.ndarray) else g.tolist()
+                                                 for g in got]})
+    with open(os.path.join(HERE, "int_derive_times.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(f"int_derive_times.json written ({len(out)} cases)")
+
+
 if __name__ == "__main__":
     cmd = sys.argv[1]
     if cmd == "alphabet":
@@ -427,5 +477,7 @@ if __name__ == "__main__":
             cmd_intmodel(t)
     elif cmd == "intspace":
         cmd_intspace()
+    elif cmd == "intderive":
+        cmd_intderive()
     else:
         raise SystemExit(__doc__)
