@@ -294,6 +294,10 @@ def main():
                                                   "FP64 matrix rate on MI355X)",
                          "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
+                         # add and max are two VALU instructions per pair (no fused form):
+                         # the instruction ceiling is half the FMA-counted FLOP/s figure
+                         "peak_valu_instr": FP64_PEAK_TFLOPS / 2,
+                         "frac_valu_instr": round(achieved / (FP64_PEAK_TFLOPS / 2), 5),
                          "traffic": traffic,
                          "traffic_note": traffic_note,
                          "kernel_ms": round(vit_avg, 4),

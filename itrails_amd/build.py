@@ -26,16 +26,21 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, diag: bool = False,
+          variant: str = "") -> str:
+    """variant: an experiment build (libitrails_hip_<variant>.so, extra flags from
+    ITR_HIPCC_FLAGS), loaded with ITR_LIB; never the product library."""
     out = OUT if not diag else OUT.replace(".so", "_diag.so")
-    if not force and not diag and not needs_build():
+    if variant:
+        out = OUT.replace(".so", f"_{variant}.so")
+    if not force and not diag and not variant and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-             "-fvisibility=hidden"]
+             "-fvisibility=hidden"] + os.environ.get("ITR_HIPCC_FLAGS", "").split()
     if diag:
         flags += ["-DITR_DIAG"]
-    tag = "_diag" if diag else ""
+    tag = "_diag" if diag else (f"_{variant}" if variant else "")
     objs, procs = [], []
     for src in SOURCES:  # one compiler per translation unit, in parallel
         obj = os.path.join(CSRC, "..", f".{os.path.splitext(src)[0]}{tag}.o")

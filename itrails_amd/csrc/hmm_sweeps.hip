@@ -263,6 +263,7 @@ struct Occ {
   static constexpr int value = wgs * ((WV + 3) / 4);
 };
 
+
 template <int QL, int WV, int RJN, int IQ, int MODE>
 __device__ __forceinline__ void sweep_device(const SweepArgs& p) {
   constexpr int W = WV;       // wavefronts per workgroup
@@ -1089,7 +1090,9 @@ static bool fits(int c, int n) { return cfg_xr(c) >= n && kCfgs[c].ql * kCfgs[c]
 // sweep runs fastest on three waves with three targets per lane (configuration 20), the
 // posterior sweeps on four waves (2), Viterbi on the one-target-per-lane kernel (9).
 static int pick_cfg(int n, int mode) {
-  const char* force = getenv("ITR_SWEEP_CFG");  // experiments: force a configuration
+  // experiments: force a configuration (ITR_VIT_CFG: the Viterbi sweep only)
+  const char* force = (mode == MODE_VIT && getenv("ITR_VIT_CFG")) ? getenv("ITR_VIT_CFG")
+                                                                  : getenv("ITR_SWEEP_CFG");
   if (force) {
     const int c = atoi(force);
     if (c >= 0 && c < kNumCfgs && fits(c, n)) return c;
@@ -1186,7 +1189,9 @@ SweepGeometry sweep_geometry(int n, int mode) {
   // the three-wave forward kernel: one workgroup per CU beyond the occupancy API's count
   // (measured on the (5,5) model, 10 Mbp: 6.0 vs 6.8 ms)
   if (g.iq == 20 && mode == MODE_FWD_LL) g.per_cu = occ + 1;
-  const char* pcu = getenv("ITR_PER_CU");  // experiments: resident workgroups per CU
+  // experiments: resident workgroups per CU (ITR_VIT_PER_CU: the Viterbi sweep only)
+  const char* pcu = (mode == MODE_VIT && getenv("ITR_VIT_PER_CU")) ? getenv("ITR_VIT_PER_CU")
+                                                                   : getenv("ITR_PER_CU");
   if (pcu && atoi(pcu) > 0) g.per_cu = atoi(pcu);
   return g;
 }

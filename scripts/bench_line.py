@@ -1,0 +1,8 @@
+"""Print one summary line of a bench.py JSON result (experiment scripts)."""
+import json
+import sys
+
+d = json.load(open(sys.argv[1]))
+r = d["roofline"]
+print(" ".join(sys.argv[2:]), round(d["value"] / 1e6, 1), "Mcol/s fwd", r.get("forward_ms"),
+      "vit", r.get("kernel_ms"), "trace", r.get("traceback_ms"), "check", d.get("check"))
