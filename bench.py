@@ -36,6 +36,30 @@ KAT = {"t_1": 240000.0 * MU, "t_2": 40000.0 * MU, "N_AB": 50000.0 * MU, "N_ABC":
        "t_upper": 745069.3855 * MU, "r": 1e-8 / MU}
 
 
+# the introgression model: the KAT set plus B/C admixture 20 kyr before
+# the first speciation, {t_1} case (t_B = t_C = t_1 - t_m, int_optimizer.py:504-520),
+# admixture proportion m = 0.1 passed as is (the int CLIs would pass m * mu)
+INT_KAT = {"t_1": 240000.0 * MU, "t_2": 40000.0 * MU, "N_AB": 50000.0 * MU,
+           "N_BC": 40000.0 * MU, "N_ABC": 50000.0 * MU, "t_upper": 745069.3855 * MU,
+           "r": 1e-8 / MU, "t_m": 20000.0 * MU, "m": 0.1}
+
+
+def load_model_intro(n_int: int):
+    """The introgression HMM built on the device (model/intro.py) before the timed region."""
+    from itrails_amd.config import derive_times_int
+    from itrails_amd.model.emissions import cutpoints_ABC
+    from itrails_amd.model.intro import trans_emiss_calc_introgression
+
+    d = dict(INT_KAT)
+    d = derive_times_int(d, frozenset(["t_1"]), cutpoints_ABC(n_int, 1)[n_int - 1])
+    t0 = time.time()
+    a, b, pi, _, _ = trans_emiss_calc_introgression(
+        d["t_A"], d["t_B"], d["t_C"], d["t_2"], d["t_upper"], d["t_out"], d["t_m"], d["N_AB"],
+        d["N_BC"], d["N_ABC"], d["r"], d["m"], n_int, n_int)
+    return a, b, pi, (f"itrails introgression ({n_int},{n_int}) model (device-built, "
+                      f"{time.time() - t0:.2f} s)")
+
+
 def load_model(n_int: int):
     f = os.path.join(ROOT, "tests", "golden", f"model_kat_{n_int}_{n_int}.npz")
     if os.path.exists(f):
@@ -65,6 +89,10 @@ def main():
                          "posterior decoding (config 3, use --n-int 7); optimize: one "
                          "itrails-optimize objective evaluation per step = device model "
                          "rebuild + forward log-likelihood of the resident columns (config 5)")
+    ap.add_argument("--model", choices=["itrails", "introgression"], default="itrails",
+                    help="itrails: the plain ILS model (BASELINE configs); introgression: "
+                         "the B/C admixture model of itrails-int-* (SURVEY 8(f) row 4), "
+                         "built on the device at startup")
     ap.add_argument("--mbp", type=float, default=10.0, help="columns per GPU (Mbp)")
     ap.add_argument("--mean-block", type=float, default=2000.0)
     ap.add_argument("--cpu-sample", type=int, default=10_000_000,
@@ -100,7 +128,8 @@ def main():
     from itrails_amd import hmm
     from itrails_amd.synth import block_lengths, sample_alignment
 
-    a, b, pi, model_name = load_model(args.n_int)
+    intro = args.model == "introgression"
+    a, b, pi, model_name = load_model_intro(args.n_int) if intro else load_model(args.n_int)
     n = a.shape[0]
     cols = int(args.mbp * 1e6)
     # identical block-length layout on every rank (weak scaling: the same work per GPU, so
@@ -143,14 +172,16 @@ def main():
         # one objective evaluation at a nearby parameter vector (the simplex moves every
         # call): model rebuild on the device, forward log-likelihood of every block,
         # all-reduce of the per-block values (N > 1), host sum in block order
-        from itrails_amd.optimizer import model_for
+        from itrails_amd.optimizer import model_for, model_for_introgression
 
         eval_no[0] += 1
-        names = list(KAT)
-        x = [KAT[k] * (1.0 + 1e-3 * ((eval_no[0] + i) % 5 - 2)) for i, k in enumerate(names)]
+        base = INT_KAT if intro else KAT
+        names = list(base)
+        x = [base[k] * (1.0 + 1e-3 * ((eval_no[0] + i) % 5 - 2)) for i, k in enumerate(names)]
         tb = time.perf_counter()
-        _, (a1, b1, p1, _, _) = model_for(x, names, frozenset(["t_1"]),
-                                          {"n_int_AB": args.n_int, "n_int_ABC": args.n_int})
+        build = model_for_introgression if intro else model_for
+        _, (a1, b1, p1, _, _) = build(x, names, frozenset(["t_1"]),
+                                      {"n_int_AB": args.n_int, "n_int_ABC": args.n_int})
         m1 = hmm.Model(a1, b1, p1)
         build_ms.append((time.perf_counter() - tb) * 1e3)
         hmm.forward_loglik_device(m1, plan, d_obs, out=d_ll)
@@ -244,7 +275,19 @@ def main():
         achieved = ops_per_col * cols / (vit_avg * 1e-3) / 1e12
         traffic, traffic_note = pmc_traffic(n, {"fv": 3, "posterior": 2, "optimize": 0}[args.mode])
         cpu = None
-        if opt_mode:
+        if opt_mode and intro:
+            # the reference's introgression build, timed when its golden model was made in
+            # the build container (tests/golden/make_golden.py intmodel; 8 cores shared)
+            f = os.path.join(ROOT, "tests", "golden",
+                             f"model_int_ikat_{args.n_int}_{args.n_int}.npz")
+            if os.path.exists(f):
+                sec = float(np.load(f)["build_seconds"])
+                cpu = {"value": round(1.0 / sec, 6), "unit": "evaluations/s", "cores": 8,
+                       "kind": "reference",
+                       "sample": f"trans_emiss_calc_introgression ({args.n_int},{args.n_int}) "
+                                 f"{sec:.0f} s in the build container, not re-timed on the "
+                                 "GPU box"}
+        elif opt_mode:
             # the reference's own model build: 615 s per (5,5) evaluation on the 8-core
             # survey container; it cannot run on the GPU box
             cpu = {"value": round(1.0 / 615.0, 6), "unit": "evaluations/s", "cores": 8,
@@ -262,6 +305,9 @@ def main():
                   "posterior": "alignment columns/s (posterior decoding), 3sp+outgroup HMM",
                   "optimize": "itrails-optimize objective evaluations/s (device model rebuild "
                               "+ forward loglik of the resident alignment)"}[args.mode]
+        if intro:
+            metric = metric.replace("3sp+outgroup HMM", "3sp+outgroup introgression HMM") \
+                .replace("itrails-optimize", "itrails-int-optimize")
         if opt_mode:
             value = args.steps / dt
         result = {
