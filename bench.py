@@ -336,14 +336,18 @@ def main():
             "roofline": {"kernel": {"fv": "sweep_kernel<VIT> (Viterbi max-plus)",
                                     "posterior": "sweep_kernel<BWD> (backward + posterior)",
                                     "optimize": "sweep_kernel<FWD_LL> (forward)"}[args.mode],
-                         "bound": "mfma", "pipe": "FP64 VALU (add/max; FP64 vector rate = "
-                                                  "FP64 matrix rate on MI355X)",
+                         "bound": "mfma",
+                         "pipe": ("FP64 VALU (add/max; FP64 vector rate = FP64 matrix rate on "
+                                  "MI355X)" if args.mode == "fv" else
+                                  "FP64 VALU FMA (FP64 vector rate = FP64 matrix rate on "
+                                  "MI355X)"),
                          "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
                          # add and max are two VALU instructions per pair (no fused form):
                          # the instruction ceiling is half the FMA-counted FLOP/s figure
-                         "peak_valu_instr": FP64_PEAK_TFLOPS / 2,
-                         "frac_valu_instr": round(achieved / (FP64_PEAK_TFLOPS / 2), 5),
+                         **({"peak_valu_instr": FP64_PEAK_TFLOPS / 2,
+                             "frac_valu_instr": round(achieved / (FP64_PEAK_TFLOPS / 2), 5)}
+                            if args.mode == "fv" else {}),
                          "traffic": traffic,
                          "traffic_note": traffic_note,
                          "kernel_ms": round(vit_avg, 4),
