@@ -22,6 +22,7 @@ on the host, in the reference's order, so key insertion order and overwrite orde
 """
 from __future__ import annotations
 
+from functools import lru_cache
 from typing import Dict, List, Tuple
 
 import numpy as np
@@ -111,8 +112,23 @@ def run_chain_ab(Q, times, masks, probs: Dict, n_int, la) -> Dict:
 
 def run_chain_abc(Q, times, ss, probs: Dict, n_int, la) -> Dict:
     """run_markov_chain_ABC.py:312-796: three-species chain, n_int - 1 finite intervals and
-    the closing deepest interval; returns {hidden-state pair: probability}."""
+    the closing deepest interval; returns {hidden-state pair: probability}.
+
+    The branching structure (which keys exist, which branch reaches which key through which
+    omega classes and Van Loan paths) depends only on n_int and the incoming keys, so it is
+    planned once (`_abc_plan`, cached: every objective evaluation of the optimizer reuses
+    it) and each build only runs the numbers: per interval one expm, one Van Loan batch,
+    one stacked GEMM for the plain branches and one per Van Loan path group."""
+    plan = _abc_plan(n_int, tuple(probs.keys()))
+    if plan is None:  # an interval whose path-by-path order matters: the dict form
+        return _run_chain_abc_dicts(Q, times, ss, probs, n_int, la)
+    return _run_chain_abc_planned(plan, Q, times, ss, probs, la)
+
+
+def _run_chain_abc_dicts(Q, times, ss, probs: Dict, n_int, la) -> Dict:
+    """run_chain_abc on dictionaries, interval by interval (the reference's form)."""
     masks = ss.omega_masks
+    fmask = {k: m.astype(np.float64) for k, m in masks.items()}
     nrc = omega_nonrev_counts(3)
     inv = INVERTED_OMEGA_NONREV_COUNTS_3
     for step in range(n_int - 1):
@@ -150,23 +166,261 @@ def run_chain_abc(Q, times, ss, probs: Dict, n_int, la) -> Dict:
         vl_list = list(vl_needed.keys())
         for p, S in zip(vl_list, la.vanloan(Q, dt, masks, vl_list)):
             vl_needed[p] = S
-        for path, plain, vl in plan:
-            pm = probs[path]
-            writes = []
-            for key, om_s, om_e in plain:
-                ms = masks[om_s].astype(np.float64)
-                me = masks[om_e].astype(np.float64)
-                writes.append((key, (pm * ms) @ E * me))
-            for key6, sub, om_s, om_e in vl:
-                S = vl_needed[sub[0]].copy()
-                for p in sub[1:]:
-                    S = S + vl_needed[p]
-                ms = masks[om_s].astype(np.float64)
-                me = masks[om_e].astype(np.float64)
-                writes.append(((key6[:3], key6[3:]), (pm * ms) @ S * me))
-            for key, v in writes:  # plain results first, then Van Loan ones
-                probs[key] = v
+        # every product of the interval as stacked row blocks: (pm * ms) @ E * me for the
+        # plain branches (one GEMM), (pm * ms) @ sum(S over the group's omega paths) * me
+        # for the Van Loan groups (one GEMM per distinct path group)
+        plain_rows, plain_out = [], []
+        vl_rows: Dict[tuple, list] = {}
+        for pi_, (path, plain, vl) in enumerate(plan):
+            pm = probs[path][0]
+            for k, (key, om_s, om_e) in enumerate(plain):
+                plain_out.append((pi_, k, om_e))
+                plain_rows.append(pm * fmask[om_s])
+            for k, (key6, sub, om_s, om_e) in enumerate(vl):
+                vl_rows.setdefault(tuple(sub), []).append((pi_, k, om_s, om_e))
+        # The reference updates path by path, so a later path reads an earlier path's write
+        # if that write lands on its key; the stacked products read every path first, which
+        # is the same only without such a hazard (otherwise: the path-by-path order).
+        pos = {path: i for i, (path, _, _) in enumerate(plan)}
+        hazard = any(pos.get(key, -1) > i for i, (path, plain, vl) in enumerate(plan)
+                     for key in [k for k, _, _ in plain] + [(k6[:3], k6[3:]) for k6, _, _, _ in vl])
+        if hazard:
+            _products_in_order(plan, probs, E, vl_needed, fmask)
+            continue
+        res_plain = {}
+        if plain_rows:
+            R = la.rowmat(np.stack(plain_rows), E)
+            for (pi_, k, om_e), row in zip(plain_out, R):
+                res_plain[(pi_, k)] = (row * fmask[om_e]).reshape(1, -1)
+        res_vl = {}
+        for sub, items in vl_rows.items():
+            S = vl_needed[sub[0]].copy()
+            for p in sub[1:]:
+                S = S + vl_needed[p]
+            V = np.stack([probs[plan[pi_][0]][0] * fmask[om_s] for pi_, _, om_s, _ in items])
+            R = V @ S
+            for (pi_, k, _, om_e), row in zip(items, R):
+                res_vl[(pi_, k)] = (row * fmask[om_e]).reshape(1, -1)
+        for pi_, (path, plain, vl) in enumerate(plan):
+            for k, (key, _, _) in enumerate(plain):  # plain results first, then Van Loan ones
+                probs[key] = res_plain[(pi_, k)]
+            for k, (key6, _, _, _) in enumerate(vl):
+                probs[(key6[:3], key6[3:])] = res_vl[(pi_, k)]
     return _close_deepest(Q, ss, probs, n_int, la)
+
+
+class _IntervalPlan:
+    __slots__ = ("vl_paths", "plain", "groups")
+
+    def __init__(self, vl_paths, plain, groups):
+        self.vl_paths = vl_paths   # distinct Van Loan omega paths of the interval
+        self.plain = plain         # (src rows, start omega ids, end omega ids, dst rows)
+        self.groups = groups       # [(path ids, src, start ids, end ids, dst)] per path group
+
+
+class _ABCPlan:
+    __slots__ = ("nrows", "omegas", "intervals", "close_paths", "close_order", "close_groups",
+                 "close_sum_rows")
+
+
+@lru_cache(maxsize=16)
+def _abc_plan(n_int: int, keys0: tuple):
+    """The structural plan of run_chain_abc for n_int intervals and the incoming keys (in
+    their order): per interval the branch table as row-index arrays, then the closing phase.
+    None if some interval has a path-by-path ordering hazard (a later path reading a key an
+    earlier path of the same interval wrote)."""
+    nrc = omega_nonrev_counts(3)
+    inv = INVERTED_OMEGA_NONREV_COUNTS_3
+    rows = {k: i for i, k in enumerate(keys0)}
+    keys = list(keys0)
+    om_ids: Dict = {}
+
+    def oid(om):
+        if om not in om_ids:
+            om_ids[om] = len(om_ids)
+        return om_ids[om]
+
+    def row_of(key):
+        if key not in rows:
+            rows[key] = len(keys)
+            keys.append(key)
+        return rows[key]
+
+    intervals = []
+    for step in range(n_int - 1):
+        og = list(keys)
+        ogs = set(og)
+        pos = {k: i for i, k in enumerate(og)}
+        writes = []  # (dst key, kind, payload) in the reference's write order
+        vl_index: Dict = {}
+        for pi_, path in enumerate(og):
+            om_s = omega_of_key(path)
+            plain, vl = [], []
+            for l in _branch_rows_abc(path[0], step):
+                lt = tuple(int(x) for x in l)
+                for r in _branch_rows_abc(path[1], step):
+                    rt = tuple(int(x) for x in r)
+                    key = (lt, rt)
+                    if key in ogs and key != path:
+                        continue
+                    om_e = omega_of_key(key)
+                    double_l = lt[0] != 0 and lt[1] == lt[2] and lt[1] != -1
+                    double_r = rt[0] != 0 and rt[1] == rt[2] and rt[1] != -1
+                    if double_l or double_r:
+                        for key6, sub in vanloan_paths(om_s, om_e, nrc, inv, lt, rt, lt, rt):
+                            for p in sub:
+                                vl_index.setdefault(p, len(vl_index))
+                            vl.append(((key6[:3], key6[3:]), ("vl", tuple(sub), om_s, om_e)))
+                    else:
+                        plain.append((key, ("plain", None, om_s, om_e)))
+            for key, how in plain + vl:
+                if pos.get(key, -1) > pi_:
+                    return None
+                writes.append((key, path, how))
+        last = {}
+        for w, (key, _, _) in enumerate(writes):  # a later write of the same key wins
+            last[key] = w
+        src_rows = [rows[path] for _, path, _ in writes]
+        dst_rows = [row_of(key) for key, _, _ in writes]
+        pl = [[], [], [], []]
+        gr: Dict = {}
+        for w, (key, path, (kind, sub, om_s, om_e)) in enumerate(writes):
+            if last[key] != w:
+                continue
+            if kind == "plain":
+                tgt = pl
+            else:
+                tgt = gr.setdefault(sub, [[], [], [], []])
+            tgt[0].append(src_rows[w])
+            tgt[1].append(oid(om_s))
+            tgt[2].append(oid(om_e))
+            tgt[3].append(dst_rows[w])
+        arr = lambda v: np.asarray(v, dtype=np.int64)  # noqa: E731
+        groups = [(arr([vl_index[p] for p in sub]), arr(g[0]), arr(g[1]), arr(g[2]), arr(g[3]))
+                  for sub, g in gr.items()]
+        intervals.append(_IntervalPlan(list(vl_index), tuple(arr(v) for v in pl), groups))
+
+    # the closing (unbounded) interval: run_markov_chain_ABC.py:512-796
+    absorbing = (7, 7)
+    last_i = n_int - 1
+    close_order = []       # (out key, "sum", sum index) / (out key, "deep", task index)
+    sum_rows = []
+    task_rows, task_subs = [], []
+    dp_index: Dict = {}
+    for path in keys:
+        l, r = path
+        row = rows[path]
+        l_done, r_done = all(x != -1 for x in l), all(x != -1 for x in r)
+        l_half = l[2] == -1 and all(x != -1 for x in l[:2])
+        r_half = r[2] == -1 and all(x != -1 for x in r[:2])
+        l_none, r_none = all(x == -1 for x in l), all(x == -1 for x in r)
+        summed = None
+        if l_done and r_done:
+            summed = path
+        elif l_done and r_half:
+            summed = (l, (r[0], r[1], last_i))
+        elif l_half and r_done:
+            summed = ((l[0], l[1], last_i), r)
+        elif l_half and r_half:
+            summed = ((l[0], l[1], last_i), (r[0], r[1], last_i))
+        if summed is not None:
+            close_order.append((tuple(tuple(int(v) for v in sd) for sd in summed), "sum",
+                                len(sum_rows)))
+            sum_rows.append(row)
+            continue
+        if l_done and r_none:
+            new = (l, (r[0], last_i, last_i))
+        elif l_half and r_none:
+            new = ((l[0], l[1], last_i), (r[0], last_i, last_i))
+        elif l_none and r_done:
+            new = ((l[0], last_i, last_i), r)
+        elif l_none and r_half:
+            new = ((l[0], last_i, last_i), (r[0], r[1], last_i))
+        elif l_none and r_none:
+            new = ((l[0], last_i, last_i), (r[0], last_i, last_i))
+        else:
+            continue  # the reference drops keys of any other shape
+        for key6, sub in deepest_paths(omega_of_key(path), absorbing, nrc, inv, new):
+            if all(x == 0 for x in key6):  # run_markov_chain_ABC.py:150 stops at a zero key
+                break
+            for p in sub:
+                dp_index.setdefault(p, len(dp_index))
+            close_order.append(((tuple(key6[:3]), tuple(key6[3:])), "deep", len(task_rows)))
+            task_rows.append(row)
+            task_subs.append(tuple(sub))
+    cg: Dict = {}
+    for t, sub in enumerate(task_subs):
+        cg.setdefault(sub, []).append(t)
+    plan = _ABCPlan()
+    plan.nrows = len(keys)
+    plan.omegas = [om for om, _ in sorted(om_ids.items(), key=lambda kv: kv[1])]
+    plan.intervals = intervals
+    plan.close_paths = list(dp_index)
+    plan.close_order = close_order
+    plan.close_sum_rows = np.asarray(sum_rows, dtype=np.int64)
+    plan.close_groups = [(np.asarray([dp_index[p] for p in sub], dtype=np.int64),
+                          np.asarray(ts, dtype=np.int64),
+                          np.asarray([task_rows[t] for t in ts], dtype=np.int64))
+                         for sub, ts in cg.items()]
+    return plan
+
+
+def _run_chain_abc_planned(plan, Q, times, ss, probs: Dict, la) -> Dict:
+    """The numbers of run_chain_abc on a structural plan: key rows of one matrix."""
+    masks = ss.omega_masks
+    n = Q.shape[0]
+    P = np.zeros((plan.nrows, n))
+    for i, v in enumerate(probs.values()):
+        P[i] = v[0]
+    F = np.stack([masks[om].astype(np.float64) for om in plan.omegas]) if plan.omegas else \
+        np.zeros((0, n))
+    for step, ip in enumerate(plan.intervals):
+        dt = times[step]
+        E = la.expm([Q * dt])[0]
+        S = la.vanloan(Q, dt, masks, ip.vl_paths) if ip.vl_paths else []
+        results = []
+        src, oms, ome, dst = ip.plain
+        if src.size:
+            results.append((dst, la.rowmat(P[src] * F[oms], E) * F[ome]))
+        for pids, src, oms, ome, dst in ip.groups:
+            M = S[pids[0]].copy()
+            for j in pids[1:]:
+                M = M + S[j]
+            results.append((dst, (P[src] * F[oms]) @ M * F[ome]))
+        for dst, R in results:  # every read above happened before these writes
+            P[dst] = R
+    absorbing = (7, 7)
+    keep = ~masks[absorbing]
+    Qn = Q[keep][:, keep]
+    masks_n = masks_without(masks, absorbing)
+    D = la.deepest(Qn, masks_n, plan.close_paths) if plan.close_paths else []
+    sums = P[plan.close_sum_rows].sum(axis=1) if plan.close_sum_rows.size else np.zeros(0)
+    deep = np.zeros(sum(len(t) for _, t, _ in plan.close_groups))
+    for pids, tasks, rws in plan.close_groups:
+        M = D[pids[0]].copy()
+        for j in pids[1:]:
+            M = M + D[j]
+        deep[tasks] = (P[rws][:, keep] @ M).sum(axis=1)
+    out: Dict = {}
+    for key, kind, k in plan.close_order:
+        out[key] = float(sums[k]) if kind == "sum" else float(deep[k])
+    return out
+
+
+def _products_in_order(plan, probs, E, vl_needed, fmask) -> None:
+    """run_markov_chain_ABC.py:407-490 path by path (reads see earlier writes)."""
+    for path, plain, vl in plan:
+        pm = probs[path]
+        writes = []
+        for key, om_s, om_e in plain:
+            writes.append((key, (pm * fmask[om_s]) @ E * fmask[om_e]))
+        for key6, sub, om_s, om_e in vl:
+            S = vl_needed[sub[0]].copy()
+            for p in sub[1:]:
+                S = S + vl_needed[p]
+            writes.append(((key6[:3], key6[3:]), (pm * fmask[om_s]) @ S * fmask[om_e]))
+        for key, v in writes:  # plain results first, then Van Loan ones
+            probs[key] = v
 
 
 def _close_deepest(Q, ss, probs: Dict, n_int, la) -> Dict:

@@ -37,6 +37,7 @@ one-sequence chain by position; both conventions are kept.
 from __future__ import annotations
 
 import itertools
+from functools import lru_cache
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -646,13 +647,15 @@ def _pool_ab_list(n):
     return out
 
 
-def _evaluate(P: _ABCPlan, Q, om, tab, tab_names, la):
-    """Batch every heavy factor on the device, then the row-vector chains on the host."""
+def _evaluate(P: _ABCPlan, cut, Q, om, tab, tab_names, la):
+    """Batch every heavy factor on the device, then the row-vector chains on the host.
+    Chains share prefixes (the same pi row through the same first intervals), so every
+    prefix's vector is computed once; every restricted matrix is sliced once."""
     n = Q.shape[0]
     nt = n - 2
     masks = {k: np.isin(np.arange(n), v) for k, v in om.items()}
     masks_t = {k: m[:nt] for k, m in masks.items()}
-    tm = [P.cut[k + 1] - P.cut[k] for k in range(P.n)][:-1]
+    tm = [cut[k + 1] - cut[k] for k in range(P.n)][:-1]
     props = la.expm([Q * t for t in tm]) if tm else []
     vl: Dict[Tuple, np.ndarray] = {}
     inf: Dict[Tuple, np.ndarray] = {}
@@ -667,7 +670,7 @@ def _evaluate(P: _ABCPlan, Q, om, tab, tab_names, la):
     for path, k in vl:
         by_k.setdefault(k, []).append(path)
     for k, paths in sorted(by_k.items()):
-        res = la.vanloan(Q, P.cut[k + 1] - P.cut[k], masks, paths)
+        res = la.vanloan(Q, cut[k + 1] - cut[k], masks, paths)
         for p, m in zip(paths, res):
             vl[(p, k)] = m
     if inf:
@@ -677,29 +680,37 @@ def _evaluate(P: _ABCPlan, Q, om, tab, tab_names, la):
             inf[p] = m
     ix = {k: np.asarray(v, dtype=np.int64) for k, v in om.items()}
     name_row = {nm: i for i, nm in enumerate(tab_names)}
+    sliced: Dict[Tuple, object] = {}
+
+    def restricted(f):
+        m = sliced.get(f)
+        if m is None:
+            if f[0] == "S":  # identity restricted to (r, c): positions of c inside r
+                pos = {s: k for k, s in enumerate(ix[f[1]])}
+                m = ("sel", np.asarray([pos[s] for s in ix[f[2]]], dtype=np.int64))
+            else:
+                M, r, c = ((props[f[1]], f[2], f[3]) if f[0] == "P" else
+                           (vl[(f[1], f[2])], f[3], f[4]) if f[0] == "VL" else
+                           (inf[f[1]], f[2], f[3]))
+                m = ("mat", M[np.ix_(ix[r], ix[c])])
+            sliced[f] = m
+        return m
+
+    prefix: Dict[Tuple, np.ndarray] = {}
     out = {}
     for key in P.order:
-        if key in out:
-            continue
         pn, chains = P.entries[key]
-        pi = tab[name_row[pn]]
         total = 0.0
         for ch in chains:
-            v = pi
-            for f in ch:
-                if f[0] == "P":
-                    M, r, c = props[f[1]], f[2], f[3]
-                elif f[0] == "S":
-                    M, r, c = None, f[1], f[2]
-                elif f[0] == "VL":
-                    M, r, c = vl[(f[1], f[2])], f[3], f[4]
-                else:
-                    M, r, c = inf[f[1]], f[2], f[3]
-                if M is None:  # identity restricted to (r, c)
-                    pos = {s: k for k, s in enumerate(ix[r])}
-                    v = v[[pos[s] for s in ix[c]]]
-                else:
-                    v = v @ M[np.ix_(ix[r], ix[c])]
+            v = tab[name_row[pn]]
+            for i in range(len(ch)):
+                pk = (pn, ch[:i + 1]) if isinstance(ch, tuple) else (pn, tuple(ch[:i + 1]))
+                w = prefix.get(pk)
+                if w is None:
+                    kind, m = restricted(ch[i])
+                    w = v[m] if kind == "sel" else v @ m
+                    prefix[pk] = w
+                v = w
             total += v.sum()
         out[key] = total
     return out
@@ -853,13 +864,21 @@ def get_joint_prob_mat_introgression(t_A, t_B, t_AB, t_C, t_m, rho_A, rho_B, rho
 
     Q3 = rate_matrix(sym3, coal_ABC, rho_ABC)
     om = abc_classes(sp3)
-    P = _ABCPlan(cut_ABC)
+    P = _abc_plan(n_int_AB, tuple(bool(c != np.inf) for c in cut_ABC))
+    return _evaluate(P, cut_ABC, Q3, om, tab, tab_names, la)
+
+
+@lru_cache(maxsize=16)
+def _abc_plan(n_int_AB: int, finite: Tuple[bool, ...]) -> "_ABCPlan":
+    """The three-sequence table as chains: structural (interval counts and which cutpoints
+    are finite), so it is planned once per model size and reused by every evaluation."""
+    P = _ABCPlan(np.array([0.0 if f else np.inf for f in finite]))
     _plan_v0_i(P, n_int_AB)
     for L, r, R in _pool_ab_list(P.n):
         _plan_ab_total(P, n_int_AB, L, r, R)
     for l, L, r, R in _pool_abc_list(P.n):
         _plan_abc_pool(P, l, L, r, R)
-    return _evaluate(P, Q3, om, tab, tab_names, la)
+    return P
 
 
 def trans_emiss_calc_introgression(t_A, t_B, t_C, t_2, t_upper, t_out, t_m, N_AB, N_BC,

@@ -114,6 +114,14 @@ class DeviceLinalg:
         self.stats["deepest"] += len(paths)
         return out
 
+    def rowmat(self, V: np.ndarray, M: np.ndarray) -> np.ndarray:
+        """V @ M for a stack of row vectors V (k x n) and one n x n propagator: the per-key
+        vector-matrix products of a chain interval as one MFMA GEMM (dense.hip)."""
+        from ..dense import gemm_batched
+        if V.shape[0] == 0:
+            return np.zeros((0, M.shape[1]))
+        return gemm_batched(np.ascontiguousarray(V)[None], np.ascontiguousarray(M)[None])[0]
+
     def emission_rows(self, tables: np.ndarray) -> np.ndarray:
         """Emission rows of every state from its packed tables (emission.hip)."""
         from .._lib import check, lib

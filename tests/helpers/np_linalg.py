@@ -41,6 +41,9 @@ class NumpyLinalg:
             out.append((-np.linalg.inv(C))[:n, -n:] @ A)
         return out
 
+    def rowmat(self, V, M):
+        return V @ M
+
     def emission_rows(self, tab):
         out = np.zeros((tab.shape[0], 256))
         for s in range(tab.shape[0]):
