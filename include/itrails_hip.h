@@ -141,6 +141,15 @@ ITR_API int itr_expm_batched(int n, int64_t batch, const double* d_A, double* d_
                              void* stream);
 ITR_API int itr_expm_batched_host(int n, int64_t batch, const double* h_A, double* h_out);
 
+/* The same for Van Loan matrices (vanloan.py:392-425): every member is block upper
+ * triangular, n_blocks x n_blocks blocks of order n_block (n = n_block * n_blocks), with
+ * all diagonal blocks equal (Q t).  Pade branch and scaling exactly as itr_expm_batched
+ * (the 1-norm of the whole member); only the blocks on and above the diagonal are formed
+ * (a product costs k(k+1)(k+2)/6 block GEMMs instead of k^3) and V - U is inverted through
+ * its one diagonal block by block back substitution.  out's lower blocks are zero. */
+ITR_API int itr_expm_blocktri_batched(int n_block, int n_blocks, int64_t batch,
+                                      const double* d_A, double* d_out, void* stream);
+
 /* Solve M_b X_b = R_b for b < batch (M n x n, R n x nrhs, row-major, contiguous batches).
  * M is overwritten by its LU factors (partial pivoting, first maximum |.| like LAPACK
  * idamax), R by X.  Replaces np.linalg.inv in deepest_ti (deepest_ti.py:256: the last n

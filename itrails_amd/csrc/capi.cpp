@@ -622,6 +622,20 @@ int itr_expm_batched(int n, int64_t batch, const double* A, double* out, void* s
   return 0;
 }
 
+int itr_expm_blocktri_batched(int n_block, int n_blocks, int64_t batch, const double* A,
+                              double* out, void* stream) {
+  if (n_block < 1 || n_blocks < 1 || batch < 0)
+    return fail(ITR_EINVAL, "bad block expm shape n_block=%d n_blocks=%d batch=%lld", n_block,
+                n_blocks, (long long)batch);
+  if (batch == 0) return 0;
+  if (!A || !out) return fail(ITR_EINVAL, "null device pointer");
+  hipStream_t st = (hipStream_t)stream;
+  Scope sc("expm", st);
+  const hipError_t e = itr::expm_blocktri_batched(n_block, n_blocks, batch, A, out, st);
+  if (e != hipSuccess) return fail(ITR_EHIP, "block expm failed: %s", hipGetErrorString(e));
+  return 0;
+}
+
 int itr_expm_batched_host(int n, int64_t batch, const double* h_A, double* h_out) {
   if (n < 1 || batch < 0) return fail(ITR_EINVAL, "bad expm shape");
   if (batch == 0) return 0;

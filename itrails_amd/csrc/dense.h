@@ -31,6 +31,12 @@ hipError_t solve_batched(int n, int nrhs, int64_t batch, double* M, double* R, i
 
 // out[b] = expm(A[b]) (expm.py:9-167).  Allocates its own workspace (stream-ordered).
 hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipStream_t st);
+// The same for members that are block upper triangular (kb x kb blocks of order nb, all
+// diagonal blocks equal; Van Loan matrices): only the blocks on and above the diagonal are
+// formed, the result's lower blocks are zero.  Same Pade branch and scaling per member
+// (the 1-norm of the whole matrix).
+hipError_t expm_blocktri_batched(int nb, int kb, int64_t batch, const double* A, double* out,
+                                 hipStream_t st);
 
 // emission rows (emission.hip): tables [n_states x 512] -> out [n_states x 256]
 hipError_t launch_emission(int n_states, const double* tables, double* out, hipStream_t st);

@@ -190,6 +190,28 @@ __global__ void __launch_bounds__(256) scatter_kernel(int64_t nn, const double* 
     d[e] = s[e];
 }
 
+// out[g] (nb x nb, contiguous) = block (0, 0) of in[g] (row stride ld, member stride NN)
+__global__ void __launch_bounds__(256) block00_kernel(int nb, int ld, int64_t NN, const double* in,
+                                                      double* out) {
+  const int64_t g = blockIdx.y;
+  const int64_t nn = (int64_t)nb * nb;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nn;
+       e += (int64_t)gridDim.x * 256)
+    out[g * nn + e] = in[g * NN + (e / nb) * ld + e % nb];
+}
+
+// zero the blocks (i > j) below the block diagonal of every member (kb x kb blocks of nb)
+__global__ void __launch_bounds__(256) zero_lower_kernel(int nb, int kb, double* M) {
+  const int64_t g = blockIdx.y;
+  const int n = nb * kb;
+  const int64_t NN = (int64_t)n * n;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < NN;
+       e += (int64_t)gridDim.x * 256) {
+    const int r = (int)(e / n), c = (int)(e % n);
+    if (r / nb > c / nb) M[g * NN + e] = 0.0;
+  }
+}
+
 // ||A||_1 = max_j sum_i |A_ij|, rows summed in order (numpy reduces axis 0 row by row)
 __global__ void __launch_bounds__(256) norm1_kernel(int n, const double* A, double* out) {
   __shared__ double red[256];
@@ -457,53 +479,123 @@ static hipError_t lincomb(int n, int64_t g, double* out, std::initializer_list<c
   return hipGetLastError();
 }
 
-// one Pade branch for a chunk of G members, all of order n, already gathered + scaled into
-// W[0]; result (before squaring) in W[2]
-static hipError_t pade_chunk(int n, int64_t G, int m, double* const W[8], int* piv,
-                             hipStream_t st) {
-  const int64_t nn = (int64_t)n * n;
-  auto M = [&](int i) { return Mat{W[i], nn, n}; };
-  const Mat none{nullptr, 0, 0};
+// Products and solves of the Pade evaluation.  kb == 1: dense n x n members.  kb > 1: every
+// member is block upper triangular with kb x kb blocks of order nb (n = kb nb) and all its
+// diagonal blocks equal — the Van Loan matrices of vanloan.py:392-425 (diagonal blocks Q t,
+// super-diagonal blocks diag(m) Q diag(m') t).  Every polynomial of such a matrix, and the
+// Pade quotient, has the same structure, so only the blocks i <= j are formed: a product
+// costs kb(kb+1)(kb+2)/6 block GEMMs instead of kb^3, and (V - U) R = V + U is solved by
+// block back substitution with the inverse of the one diagonal block instead of an LU of
+// order n.  Blocks below the diagonal of the work buffers are never read.
+struct PadeOps {
+  int n, nb, kb;
+  hipStream_t st;
+  double* inv;  // kb > 1: [G][nb][nb] inverse of the diagonal block of V - U
+  double* tmp;  // kb > 1: [G][nb][nb] its LU copy
+  int* piv;
+
+  Mat blk(double* base, int i, int j) const {
+    const int64_t NN = (int64_t)n * n;
+    return Mat{base + (int64_t)i * nb * n + (int64_t)j * nb, NN, n};
+  }
+  // Z = alpha X Y + beta D + gamma I  (members selected by idx when given)
+  hipError_t mul(double* X, double* Y, double* Z, double alpha, double* D, double beta,
+                 double gamma, const int* idx, int64_t G) const {
+    const int64_t NN = (int64_t)n * n;
+    const Mat none{nullptr, 0, 0};
+    if (kb == 1)
+      return gemm(n, n, n, Mat{X, NN, n}, Mat{Y, NN, n}, Mat{Z, NN, n}, alpha,
+                  D ? Mat{D, NN, n} : none, beta, gamma, idx, G, st);
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < kb && !e; ++i)
+      for (int j = i; j < kb && !e; ++j)
+        for (int l = i; l <= j && !e; ++l) {
+          const bool first = l == i;  // later terms accumulate into Z_ij
+          e = gemm(nb, nb, nb, blk(X, i, l), blk(Y, l, j), blk(Z, i, j), alpha,
+                   first ? (D ? blk(D, i, j) : none) : blk(Z, i, j), first ? beta : 1.0,
+                   (first && i == j) ? gamma : 0.0, idx, G, st);
+        }
+    return e;
+  }
+  // M R = N for every member; R returned in `R` (kb == 1: R == N, overwritten; M
+  // overwritten by its LU factors)
+  hipError_t solve(double* M, double* N, double* R, int64_t G) const {
+    if (kb == 1) return solve_batched(n, n, G, M, N, piv, st);
+    const int64_t NN = (int64_t)n * n, bnn = (int64_t)nb * nb;
+    const Mat none{nullptr, 0, 0};
+    hipError_t e = hipSuccess;
+    const int bx = (int)std::min<int64_t>((bnn + 255) / 256, 64);
+    for (int64_t g0 = 0; !e && g0 < G; g0 += 65535) {
+      hipLaunchKernelGGL(block00_kernel, dim3(bx, (unsigned)std::min<int64_t>(65535, G - g0)),
+                         dim3(256), 0, st, nb, n, NN, M + g0 * NN, tmp + g0 * bnn);
+      e = hipGetLastError();
+    }
+    if (!e) e = lincomb(nb, G, inv, {}, {}, 1.0, st);       // identity
+    if (!e) e = solve_batched(nb, nb, G, tmp, inv, piv, st);  // inverse of the diagonal block
+    for (int j = 0; j < kb && !e; ++j)
+      for (int i = j; i >= 0 && !e; --i) {
+        // N_ij -= sum_{l > i} M_il R_lj, then R_ij = inv N_ij
+        for (int l = i + 1; l <= j && !e; ++l)
+          e = gemm(nb, nb, nb, blk(M, i, l), blk(R, l, j), blk(N, i, j), -1.0, blk(N, i, j),
+                   1.0, 0.0, nullptr, G, st);
+        if (!e)
+          e = gemm(nb, nb, nb, Mat{inv, bnn, nb}, blk(N, i, j), blk(R, i, j), 1.0, none, 0.0,
+                   0.0, nullptr, G, st);
+      }
+    return e;
+  }
+};
+
+// one Pade branch for a chunk of G members, already gathered + scaled into W[0]; result
+// (before squaring) in W[2]
+static hipError_t pade_chunk(const PadeOps& O, int64_t G, int m, double* const W[8]) {
+  const int n = O.n;
   hipError_t e;
 #define TRY(x)                   \
   if ((e = (x)) != hipSuccess) { \
     return e;                    \
   }
   // A2 = A @ A
-  TRY(gemm(n, n, n, M(0), M(0), M(1), 1.0, none, 0.0, 0.0, nullptr, G, st));
+  TRY(O.mul(W[0], W[0], W[1], 1.0, nullptr, 0.0, 0.0, nullptr, G));
   if (m == 13) {
     const double* b = kB13;
-    TRY(gemm(n, n, n, M(1), M(1), M(2), 1.0, none, 0.0, 0.0, nullptr, G, st));  // A4
-    TRY(gemm(n, n, n, M(1), M(2), M(3), 1.0, none, 0.0, 0.0, nullptr, G, st));  // A6 = A2 A4
+    TRY(O.mul(W[1], W[1], W[2], 1.0, nullptr, 0.0, 0.0, nullptr, G));  // A4
+    TRY(O.mul(W[1], W[2], W[3], 1.0, nullptr, 0.0, 0.0, nullptr, G));  // A6 = A2 A4
     // U = A (A6 (b13 A6 + b11 A4 + b9 A2) + b7 A6 + b5 A4 + b3 A2 + b1 I)
-    TRY(lincomb(n, G, W[4], {W[3], W[2], W[1]}, {b[13], b[11], b[9]}, 0.0, st));
-    TRY(lincomb(n, G, W[5], {W[3], W[2], W[1]}, {b[7], b[5], b[3]}, b[1], st));
-    TRY(gemm(n, n, n, M(3), M(4), M(6), 1.0, M(5), 1.0, 0.0, nullptr, G, st));
-    TRY(gemm(n, n, n, M(0), M(6), M(7), 1.0, none, 0.0, 0.0, nullptr, G, st));  // U -> W7
+    TRY(lincomb(n, G, W[4], {W[3], W[2], W[1]}, {b[13], b[11], b[9]}, 0.0, O.st));
+    TRY(lincomb(n, G, W[5], {W[3], W[2], W[1]}, {b[7], b[5], b[3]}, b[1], O.st));
+    TRY(O.mul(W[3], W[4], W[6], 1.0, W[5], 1.0, 0.0, nullptr, G));
+    TRY(O.mul(W[0], W[6], W[7], 1.0, nullptr, 0.0, 0.0, nullptr, G));  // U -> W7
     // V = A6 (b12 A6 + b10 A4 + b8 A2) + b6 A6 + b4 A4 + b2 A2 + b0 I
-    TRY(lincomb(n, G, W[4], {W[3], W[2], W[1]}, {b[12], b[10], b[8]}, 0.0, st));
-    TRY(lincomb(n, G, W[5], {W[3], W[2], W[1]}, {b[6], b[4], b[2]}, b[0], st));
-    TRY(gemm(n, n, n, M(3), M(4), M(6), 1.0, M(5), 1.0, 0.0, nullptr, G, st));  // V -> W6
+    TRY(lincomb(n, G, W[4], {W[3], W[2], W[1]}, {b[12], b[10], b[8]}, 0.0, O.st));
+    TRY(lincomb(n, G, W[5], {W[3], W[2], W[1]}, {b[6], b[4], b[2]}, b[0], O.st));
+    TRY(O.mul(W[3], W[4], W[6], 1.0, W[5], 1.0, 0.0, nullptr, G));  // V -> W6
   } else {
     const double* b = m == 3 ? kB3 : m == 5 ? kB5 : m == 7 ? kB7 : kB9;
     const int np = m / 2;  // powers A2 .. A^(2 np) in W1 .. W(np)  (A2n = A2n @ A2)
     for (int p = 2; p <= np; ++p)
-      TRY(gemm(n, n, n, M(p - 1), M(1), M(p), 1.0, none, 0.0, 0.0, nullptr, G, st));
+      TRY(O.mul(W[p - 1], W[1], W[p], 1.0, nullptr, 0.0, 0.0, nullptr, G));
     // U = A (b1 I + b3 A2 + ...), V = b0 I + b2 A2 + ...
     const double* P[4] = {W[1], np >= 2 ? W[2] : nullptr, np >= 3 ? W[3] : nullptr,
                           np >= 4 ? W[4] : nullptr};
     TRY(lincomb(n, G, W[5], {P[0], P[1], P[2], P[3]},
                 {b[3], np >= 2 ? b[5] : 0.0, np >= 3 ? b[7] : 0.0, np >= 4 ? b[9] : 0.0},
-                b[1], st));
-    TRY(gemm(n, n, n, M(0), M(5), M(7), 1.0, none, 0.0, 0.0, nullptr, G, st));  // U -> W7
+                b[1], O.st));
+    TRY(O.mul(W[0], W[5], W[7], 1.0, nullptr, 0.0, 0.0, nullptr, G));  // U -> W7
     TRY(lincomb(n, G, W[6], {P[0], P[1], P[2], P[3]},
                 {b[2], np >= 2 ? b[4] : 0.0, np >= 3 ? b[6] : 0.0, np >= 4 ? b[8] : 0.0},
-                b[0], st));  // V -> W6
+                b[0], O.st));  // V -> W6
   }
   // r = solve(V - U, V + U)  (expm.py:53,166)
-  TRY(lincomb(n, G, W[1], {W[6], W[7]}, {1.0, -1.0}, 0.0, st));
-  TRY(lincomb(n, G, W[2], {W[6], W[7]}, {1.0, 1.0}, 0.0, st));
-  TRY(solve_batched(n, n, G, W[1], W[2], piv, st));
+  TRY(lincomb(n, G, W[1], {W[6], W[7]}, {1.0, -1.0}, 0.0, O.st));
+  TRY(lincomb(n, G, W[2], {W[6], W[7]}, {1.0, 1.0}, 0.0, O.st));
+  if (O.kb == 1) {
+    TRY(O.solve(W[1], W[2], W[2], G));
+  } else {  // R in W3, then back to W2 where the squarings start
+    TRY(O.solve(W[1], W[2], W[3], G));
+    TRY(hipMemcpyAsync(W[2], W[3], (size_t)G * n * n * sizeof(double),
+                       hipMemcpyDeviceToDevice, O.st));
+  }
 #undef TRY
   return hipSuccess;
 }
@@ -522,7 +614,14 @@ static void branch_of(double norm, int* m, int* s) {
 }
 
 hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipStream_t st) {
+  return expm_blocktri_batched(n, 1, batch, A, out, st);
+}
+
+hipError_t expm_blocktri_batched(int nb, int kb, int64_t batch, const double* A, double* out,
+                                 hipStream_t st) {
   if (batch <= 0) return hipSuccess;
+  if (nb <= 0 || kb <= 0) return hipErrorInvalidValue;
+  const int n = nb * kb;
   const int64_t nn = (int64_t)n * n;
   hipError_t e;
   double* d_norm = nullptr;
@@ -540,7 +639,9 @@ hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipS
   for (int64_t b = 0; b < batch; ++b) branch_of(norm[b], &m[b], &s[b]);
 
   // chunk size: 8 work matrices per member, at most ~4 GiB of workspace per chunk
-  const int64_t per = 8 * nn * (int64_t)sizeof(double) + n * (int64_t)sizeof(int) + 64;
+  const int64_t bnn = (int64_t)nb * nb;
+  const int64_t per = 8 * nn * (int64_t)sizeof(double) + n * (int64_t)sizeof(int) + 64 +
+                      (kb > 1 ? 2 * bnn * (int64_t)sizeof(double) : 0);
   const int64_t cap = std::max<int64_t>(1, ((int64_t)4 << 30) / per);
   for (int mm : {3, 5, 7, 9, 13}) {
     std::vector<int> members;
@@ -561,7 +662,8 @@ hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipS
       }
       char* ws = nullptr;
       const size_t bytes = (size_t)(8 * G * nn) * sizeof(double) + (size_t)G * n * sizeof(int) +
-                           (size_t)G * (3 * sizeof(int) + sizeof(double)) + 256;
+                           (size_t)G * (3 * sizeof(int) + sizeof(double)) + 256 +
+                           (kb > 1 ? (size_t)(2 * G * bnn) * sizeof(double) : 0);
       if ((e = hipMallocAsync((void**)&ws, bytes, st))) return e;
       double* W[8];
       for (int i = 0; i < 8; ++i) W[i] = (double*)ws + (int64_t)i * G * nn;
@@ -570,6 +672,8 @@ hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipS
       int* d_sel = d_src + G;
       int* d_act = d_sel + G;
       double* d_scale = (double*)(((uintptr_t)(d_act + G) + 15) & ~(uintptr_t)15);
+      PadeOps O{n, nb, kb, st, kb > 1 ? d_scale + G : nullptr,
+                kb > 1 ? d_scale + G + G * bnn : nullptr, piv};
       e = hipMemcpyAsync(d_src, src.data(), G * sizeof(int), hipMemcpyHostToDevice, st);
       if (!e)
         e = hipMemcpyAsync(d_scale, scale.data(), G * sizeof(double), hipMemcpyHostToDevice, st);
@@ -580,7 +684,7 @@ hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipS
                            st, nn, A, d_src + g0, d_scale + g0, W[0] + g0 * nn);
         e = hipGetLastError();
       }
-      if (!e) e = pade_chunk(n, G, mm, W, piv, st);
+      if (!e) e = pade_chunk(O, G, mm, W);
       // s squarings, in lock-step: after level k the members with s >= k hold r^(2^k) in
       // W[2 + (k & 1)]  (np.linalg.matrix_power(r, 2**s), expm.py:167)
       for (int lev = 1; !e && lev <= smax; ++lev) {
@@ -590,11 +694,9 @@ hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipS
         e = hipMemcpyAsync(d_act, act.data(), act.size() * sizeof(int), hipMemcpyHostToDevice,
                            st);
         if (!e) e = hipStreamSynchronize(st);  // act is reused next level
-        const Mat X{W[2 + ((lev - 1) & 1)], nn, n};
-        const Mat Y{W[2 + (lev & 1)], nn, n};
-        if (!e)
-          e = gemm(n, n, n, X, X, Y, 1.0, Mat{nullptr, 0, 0}, 0.0, 0.0, d_act,
-                   (int64_t)act.size(), st);
+        double* X = W[2 + ((lev - 1) & 1)];
+        double* Y = W[2 + (lev & 1)];
+        if (!e) e = O.mul(X, X, Y, 1.0, nullptr, 0.0, 0.0, d_act, (int64_t)act.size());
       }
       for (int64_t g = 0; g < G; ++g) sel[g] = s[members[c0 + g]] & 1;
       if (!e) e = hipMemcpyAsync(d_sel, sel.data(), G * sizeof(int), hipMemcpyHostToDevice, st);
@@ -610,6 +712,14 @@ hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipS
       if (e) return e;
       if (e2) return e2;
     }
+  }
+  if (kb > 1) {  // the blocks below the block diagonal were never formed: they are zero
+    const int bx = (int)std::min<int64_t>((nn + 255) / 256, 64);
+    for (int64_t b0 = 0; b0 < batch; b0 += 65535)
+      hipLaunchKernelGGL(zero_lower_kernel,
+                         dim3(bx, (unsigned)std::min<int64_t>(65535, batch - b0)), dim3(256),
+                         0, st, nb, kb, out + b0 * nn);
+    if (hipError_t e = hipGetLastError()) return e;
   }
   return hipSuccess;
 }

@@ -18,7 +18,7 @@ import numpy as np
 
 from ._lib import check, lib
 
-__all__ = ["expm", "expm_batched", "solve_batched", "gemm_batched"]
+__all__ = ["expm", "expm_batched", "expm_blocktri_batched", "solve_batched", "gemm_batched"]
 
 
 def _dev(x):
@@ -45,6 +45,21 @@ def expm_batched(A):
     if d.shape[0]:
         check(lib().itr_expm_batched(d.shape[1], d.shape[0], d.data_ptr(), out.data_ptr(),
                                      _stream()))
+    return out if on_dev else out.cpu().numpy()
+
+
+def expm_blocktri_batched(A, n_blocks: int):
+    """expm of every A[b] whose n_blocks x n_blocks block structure is upper triangular with
+    equal diagonal blocks (Van Loan matrices, vanloan.py:392-425): same result as
+    expm_batched, only the upper blocks are formed (lower blocks of the result are zero)."""
+    import torch
+    d, on_dev = _dev(A)
+    if d.dim() != 3 or d.shape[1] != d.shape[2] or d.shape[1] % n_blocks:
+        raise ValueError("expected a (batch, k*n, k*n) array")
+    out = torch.empty_like(d)
+    if d.shape[0]:
+        check(lib().itr_expm_blocktri_batched(d.shape[1] // n_blocks, n_blocks, d.shape[0],
+                                              d.data_ptr(), out.data_ptr(), _stream()))
     return out if on_dev else out.cpu().numpy()
 
 

@@ -68,8 +68,10 @@ class DeviceLinalg:
 
     def vanloan(self, Q: np.ndarray, t: float, masks: Dict[Omega, np.ndarray],
                 paths: Sequence[Tuple[Omega, ...]]) -> List[np.ndarray]:
-        """expm(C t)[:n, -n:] for each omega path (vanloan.py:392-425)."""
-        from ..dense import expm_batched
+        """expm(C t)[:n, -n:] for each omega path (vanloan.py:392-425); C is block upper
+        bidiagonal with Q on the diagonal, so the block-triangular expm forms only the upper
+        blocks."""
+        from ..dense import expm_blocktri_batched
         n = Q.shape[0]
         out: List[np.ndarray] = [None] * len(paths)
         by_len: Dict[int, List[int]] = {}
@@ -77,7 +79,7 @@ class DeviceLinalg:
             by_len.setdefault(len(p), []).append(i)
         for L, idx in sorted(by_len.items()):
             C = self._block_matrices(Q, masks, [paths[i] for i in idx], L, float(t), L)
-            E = expm_batched(C)[:, :n, -n:].cpu().numpy()
+            E = expm_blocktri_batched(C, L)[:, :n, -n:].cpu().numpy()
             for k, i in enumerate(idx):
                 out[i] = E[k]
         self.stats["vanloan"] += len(paths)

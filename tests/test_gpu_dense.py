@@ -69,3 +69,42 @@ def test_gemm_matches_blas(gpu, m, n, k):
     B = rng.standard_normal((3, k, n))
     C = gemm_batched(A, B, alpha=-2.0)
     assert np.allclose(C, -2.0 * A @ B, rtol=1e-12, atol=1e-12 * k)
+
+
+def _vanloan_like(rng, n, k, scale):
+    """Block upper bidiagonal k x k blocks: a rate matrix Q (rows sum to 0) on the diagonal,
+    masked copies of Q above it (vanloan.py:392-425), times `scale`."""
+    Q = rng.random((n, n)) * (rng.random((n, n)) < 0.2)
+    np.fill_diagonal(Q, 0.0)
+    np.fill_diagonal(Q, -Q.sum(axis=1))
+    C = np.zeros((n * k, n * k))
+    for b in range(k):
+        C[b * n:(b + 1) * n, b * n:(b + 1) * n] = Q
+    for b in range(1, k):
+        m0, m1 = rng.random(n) < 0.5, rng.random(n) < 0.5
+        C[(b - 1) * n:b * n, b * n:(b + 1) * n] = m0[:, None] * Q * m1[None, :]
+    return C * scale
+
+
+@pytest.mark.parametrize("n,k", [(5, 2), (17, 3), (40, 4), (64, 5), (70, 2)])
+def test_expm_blocktri_matches_dense(gpu, n, k):
+    """Block-triangular Van Loan expm (only the upper blocks formed, back substitution
+    through the diagonal block) against the dense batched expm and scipy, every Pade branch
+    (norms from 1e-3 to 30)."""
+    import scipy.linalg as sl
+    from itrails_amd.dense import expm_batched, expm_blocktri_batched
+    rng = np.random.default_rng(n * 10 + k)
+    A = np.stack([_vanloan_like(rng, n, k, s) for s in (1e-3, 0.05, 0.3, 0.7, 1.5, 4.0, 30.0)])
+    B = expm_blocktri_batched(A, k)
+    D = expm_batched(A)
+    for b in range(A.shape[0]):
+        ref = sl.expm(A[b])
+        for i in range(k):
+            for j in range(k):
+                blk = np.s_[i * n:(i + 1) * n, j * n:(j + 1) * n]
+                if i > j:
+                    assert not B[b][blk].any()
+                    continue
+                scale = max(np.abs(ref[blk]).max(), 1e-300)
+                assert np.abs(B[b][blk] - D[b][blk]).max() <= 1e-12 * max(scale, 1.0)
+                assert np.abs(B[b][blk] - ref[blk]).max() <= 1e-11 * max(scale, 1.0)
