@@ -61,22 +61,32 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
 
   const int ar = tid >> 2, ak = (tid & 3) * 4;   // A tile: row ar, k ak..ak+3
   const int bk = tid >> 4, bc = (tid & 15) * 4;  // B tile: k bk, cols bc..bc+3
+  // the next K tile is fetched into registers while the current one is multiplied out of
+  // LDS, so a tile's global-load latency hides behind the previous tile's MFMAs
+  double ra[4], rb[4];
+  auto fetch = [&](int k0) {
+    const int gr = row0 + ar;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int gk = k0 + ak + e;
+      ra[e] = (gr < g.m && gk < g.k) ? A[(int64_t)gr * g.A.ld + gk] : 0.0;
+    }
+    const int gk = k0 + bk;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int gc = col0 + bc + e;
+      rb[e] = (gk < g.k && gc < g.n) ? B[(int64_t)gk * g.B.ld + gc] : 0.0;
+    }
+  };
+  fetch(0);
   for (int k0 = 0; k0 < g.k; k0 += GBK) {
-    {
-      const int gr = row0 + ar;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int gk = k0 + ak + e;
-        As[ak + e][ar] = (gr < g.m && gk < g.k) ? A[(int64_t)gr * g.A.ld + gk] : 0.0;
-      }
-      const int gk = k0 + bk;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int gc = col0 + bc + e;
-        Bs[bk][bc + e] = (gk < g.k && gc < g.n) ? B[(int64_t)gk * g.B.ld + gc] : 0.0;
-      }
+    for (int e = 0; e < 4; ++e) {
+      As[ak + e][ar] = ra[e];
+      Bs[bk][bc + e] = rb[e];
     }
     __syncthreads();
+    if (k0 + GBK < g.k) fetch(k0 + GBK);
 #pragma unroll
     for (int kk = 0; kk < GBK; kk += 4) {
       // v_mfma_f64_16x16x4: lane l holds A[l&15][l>>4] and B[l>>4][l&15]
