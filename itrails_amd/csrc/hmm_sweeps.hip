@@ -1088,7 +1088,8 @@ static bool fits(int c, int n) { return cfg_xr(c) >= n && kCfgs[c].ql * kCfgs[c]
 
 // Measured on the (5,5) model (N = 70), 10 Mbp: the forward log-likelihood
 // sweep runs fastest on three waves with three targets per lane (configuration 20), the
-// posterior sweeps on four waves (2), Viterbi on the one-target-per-lane kernel (9).
+// posterior sweeps on four waves (2), Viterbi on the one-target-per-lane kernel (9); for
+// 72 < N <= 144 see below.
 static int pick_cfg(int n, int mode) {
   // experiments: force a configuration (ITR_VIT_CFG: the Viterbi sweep only)
   const char* force = (mode == MODE_VIT && getenv("ITR_VIT_CFG")) ? getenv("ITR_VIT_CFG")
@@ -1098,6 +1099,13 @@ static int pick_cfg(int n, int mode) {
     if (c >= 0 && c < kNumCfgs && fits(c, n)) return c;
   }
   if (n > 64 && n <= 72) return mode == MODE_VIT ? 9 : (mode == MODE_FWD_LL ? 20 : 2);
+  // measured on the (7,7) model (N = 133, 10 Mbp, scripts/gpu_cfg133.sh): six waves with
+  // three targets per lane for the probability sweeps (posterior 146 -> 175 M columns/s),
+  // nine waves with four lanes per target for Viterbi (40.7 -> 26.0 ms)
+  if (n > 128 && n <= 144) return mode == MODE_VIT ? 17 : 21;
+  // introgression (5,5) model, N = 95 (scripts/gpu_cfg95.sh): Viterbi on six waves with four
+  // lanes per target (11.9 -> 11.0 ms); the probability sweeps keep configuration 3
+  if (n > 72 && n <= 96 && mode == MODE_VIT) return 16;
   for (int c = 0; c < kNarrow; ++c)
     if (fits(c, n)) return c;
   return -1;
