@@ -1,0 +1,104 @@
+"""The hot path at BASELINE.json's full size (config 2: the (5,5) model, 10 Mbp in geometric
+blocks of mean 2 kbp, 5,036 blocks, longest 18,377 columns) checked through properties that
+do not need the CPU oracle to run over all of it:
+
+  * the longest blocks (which the forward sweep splits into a forward and a backward half,
+    meet in the middle) and a seeded sample of the rest against the oracle: log-likelihoods
+    within 1e-8 relative, Viterbi paths identical;
+  * the split forward against the unsplit one on every split block (ITR_SPLIT_FRAC=0 at
+    plan creation): the same value to 1e-12 relative;
+  * every block's log-likelihood finite and negative, the total equal to the block-order
+    sum of the per-block values (loglik_wrapper semantics);
+  * every posterior row sums to 1 (1e-12) and matches the oracle on the sampled blocks.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden
+from itrails_amd import hmm
+from itrails_amd.synth import block_lengths, sample_alignment
+from itrails_amd.tables import build_tables
+from oracle import hmm_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def full(gpu):
+    import torch
+    g = golden("model_kat_5_5.npz")
+    a, b, pi = g["a"], g["b"], g["pi"]
+    rng = np.random.default_rng(12345)  # bench.py's layout
+    lengths = block_lengths(rng, 10_000_000, 2000.0)
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=777)
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).cuda()
+    ll = hmm.forward_loglik_device(model, plan, d_obs).cpu().numpy()
+    path = hmm.viterbi_device(model, plan, d_obs).cpu().numpy()
+    lens = np.diff(off)
+    srng = np.random.default_rng(5)
+    longest = np.argsort(-lens, kind="stable")[:12]
+    sample = np.unique(np.concatenate([longest, srng.choice(len(lens), 60, replace=False)]))
+    return dict(a=a, b=b, pi=pi, obs=obs, off=off, model=model, d_obs=d_obs, ll=ll,
+                path=path, sample=sample, longest=longest, t=build_tables(a, b, pi))
+
+
+def _sub(obs, off, blocks):
+    parts = [obs[off[k]:off[k + 1]] for k in blocks]
+    sub_off = np.zeros(len(blocks) + 1, dtype=np.int64)
+    sub_off[1:] = np.cumsum([len(p) for p in parts])
+    return np.concatenate(parts), sub_off
+
+
+def test_full_size_layout(full):
+    assert full["off"][-1] == 10_000_000
+    assert len(full["off"]) - 1 == 5036
+    assert np.diff(full["off"]).max() == 18377
+
+
+def test_full_size_sample_vs_oracle(full):
+    obs, off, sample = full["obs"], full["off"], full["sample"]
+    so, soff = _sub(obs, off, sample)
+    ll_ref = O.forward_loglik(full["t"], so, soff)
+    np.testing.assert_allclose(full["ll"][sample], ll_ref, rtol=1e-8, atol=0)
+    path_ref = O.viterbi(full["t"], so, soff)
+    got = np.concatenate([full["path"][off[k]:off[k + 1]] for k in sample])
+    np.testing.assert_array_equal(got, path_ref)
+
+
+def test_full_size_split_forward_matches_unsplit(full, monkeypatch):
+    monkeypatch.setenv("ITR_SPLIT_FRAC", "0")  # read by itr_plan_create
+    plan = hmm.Plan(full["off"])
+    ll = hmm.forward_loglik_device(full["model"], plan, full["d_obs"]).cpu().numpy()
+    k = full["longest"]
+    np.testing.assert_allclose(full["ll"][k], ll[k], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(full["ll"], ll, rtol=1e-12, atol=0)
+
+
+def test_full_size_loglik_properties(full):
+    ll = full["ll"]
+    assert np.isfinite(ll).all() and (ll < 0).all()
+    acc = 0.0
+    for v in ll.tolist():
+        acc += v
+    V = [full["obs"][full["off"][k]:full["off"][k + 1]].astype(np.int64)
+         for k in range(len(full["off"]) - 1)]
+    assert hmm.loglik_wrapper(full["a"], full["b"], full["pi"], V) == acc
+
+
+def test_full_size_posterior_rows(full):
+    import torch
+    plan = hmm.Plan(full["off"])
+    plan.reserve(full["a"].shape[0], posterior=True)
+    post = hmm.posterior_device(full["model"], plan, full["d_obs"])
+    sums = post.sum(dim=1)
+    assert float((sums - 1.0).abs().max()) < 1e-12
+    obs, off, sample = full["obs"], full["off"], full["sample"][:20]
+    so, soff = _sub(obs, off, sample)
+    ref = O.posterior(full["t"], so, soff)
+    rows = torch.cat([post[off[k]:off[k + 1]] for k in sample]).cpu().numpy()
+    np.testing.assert_allclose(rows, ref, rtol=1e-8, atol=1e-300)
+    del post
+    torch.cuda.empty_cache()
