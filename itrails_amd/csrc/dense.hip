@@ -53,6 +53,12 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int wr = w >> 1, wc = w & 1;  // this wave's 32x32 quadrant of the tile
 
+  bool row_live[2], col_live[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    row_live[i] = row0 + wr * 32 + i * 16 < g.m;
+    col_live[i] = col0 + wc * 32 + i * 16 < g.n;
+  }
   dbl4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -95,11 +101,15 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs g) {
       for (int i = 0; i < 2; ++i) a[i] = As[kk + (l >> 4)][wr * 32 + i * 16 + (l & 15)];
 #pragma unroll
       for (int j = 0; j < 2; ++j) b[j] = Bs[kk + (l >> 4)][wc * 32 + j * 16 + (l & 15)];
+      // 16 x 16 sub-tiles wholly outside C (the edge tiles of an order-203 block: 13 of 16
+      // row and column groups are real) are skipped: a wave-uniform branch, the SIMD's
+      // matrix pipe goes to the co-resident workgroups instead
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+          if (row_live[i] && col_live[j])
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
   }
