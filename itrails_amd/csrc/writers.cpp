@@ -223,11 +223,13 @@ int write_posterior_csv(const char* path, const double* post, int n_states, cons
   const int nt = std::max(1, std::min(threads > 0 ? threads : 16,
                                       (int)std::thread::hardware_concurrency()));
   const int64_t chunk = 1 << 14;  // rows per formatting task
-  std::vector<std::string> buf(nt);
-  for (int64_t r0 = 0; r0 < total; r0 += chunk * nt) {
+  // two rounds of per-thread buffers: the workers format round k + 1 while this thread
+  // writes round k, so the (serial) file writes overlap the (parallel) formatting
+  std::vector<std::string> cur(nt), nxt(nt);
+  auto launch = [&](int64_t r0, std::vector<std::string>& buf) {
     std::vector<std::thread> th;
     for (int t = 0; t < nt; ++t) {
-      th.emplace_back([&, t] {
+      th.emplace_back([&, r0, t] {
         std::string& s = buf[t];
         s.clear();
         const int64_t a = r0 + t * chunk, b = std::min(total, a + chunk);
@@ -249,9 +251,17 @@ int write_posterior_csv(const char* path, const double* post, int n_states, cons
         }
       });
     }
+    return th;
+  };
+  const int64_t step = chunk * nt;
+  std::vector<std::thread> th = launch(0, cur);
+  for (int64_t r0 = 0; r0 < total; r0 += step) {
     for (auto& x : th) x.join();
-    for (int t = 0; t < nt; ++t) fwrite(buf[t].data(), 1, buf[t].size(), fh.f);
+    th = r0 + step < total ? launch(r0 + step, nxt) : std::vector<std::thread>();
+    for (int t = 0; t < nt; ++t) fwrite(cur[t].data(), 1, cur[t].size(), fh.f);
+    std::swap(cur, nxt);
   }
+  for (auto& x : th) x.join();
   if (ferror(fh.f)) {
     *err = "write failed";
     return 1;
