@@ -1088,8 +1088,7 @@ static bool fits(int c, int n) { return cfg_xr(c) >= n && kCfgs[c].ql * kCfgs[c]
 
 // Measured on the (5,5) model (N = 70), 10 Mbp: the forward log-likelihood
 // sweep runs fastest on three waves with three targets per lane (configuration 20), the
-// posterior sweeps on four waves (2), Viterbi on the one-target-per-lane kernel (9); for
-// 72 < N <= 144 see below.
+// posterior sweeps too, Viterbi on the one-target-per-lane kernel (9); other sizes below.
 static int pick_cfg(int n, int mode) {
   // experiments: force a configuration (ITR_VIT_CFG: the Viterbi sweep only)
   const char* force = (mode == MODE_VIT && getenv("ITR_VIT_CFG")) ? getenv("ITR_VIT_CFG")
@@ -1098,7 +1097,12 @@ static int pick_cfg(int n, int mode) {
     const int c = atoi(force);
     if (c >= 0 && c < kNumCfgs && fits(c, n)) return c;
   }
-  if (n > 64 && n <= 72) return mode == MODE_VIT ? 9 : (mode == MODE_FWD_LL ? 20 : 2);
+  // (posterior sweeps at N = 70 on configuration 20: 465 -> 496 M columns/s,
+  // scripts/gpu_cfgsmall.sh)
+  if (n > 64 && n <= 72) return mode == MODE_VIT ? 9 : 20;
+  // Viterbi at 32 < N <= 64 on eight waves, one target per lane ((4,4) model, N = 46:
+  // 7.3 -> 6.2 ms)
+  if (n > 32 && n <= 64 && mode == MODE_VIT) return 8;
   // measured on the (7,7) model (N = 133, 10 Mbp, scripts/gpu_cfg133.sh): six waves with
   // three targets per lane for the probability sweeps (posterior 146 -> 175 M columns/s),
   // nine waves with four lanes per target for Viterbi (40.7 -> 26.0 ms)
