@@ -15,7 +15,7 @@ import shutil
 import sys
 
 
-def main(prof_dir, tag, out_dir="profiles"):
+def main(prof_dir, tag, n_states=None, out_dir="profiles"):
     os.makedirs(out_dir, exist_ok=True)
     stats = os.path.join(prof_dir, "trace_kernel_stats.csv")
     shutil.copy(stats, os.path.join(out_dir, f"{tag}_kernel_stats.csv"))
@@ -34,9 +34,12 @@ def main(prof_dir, tag, out_dir="profiles"):
         if "FETCH_SIZE_KiB" in d and "WRITE_SIZE_KiB" in d:
             d["hbm_bytes_raw"] = 1024 * (d["FETCH_SIZE_KiB"] + d["WRITE_SIZE_KiB"])
             d["hbm_bytes_fetch_x2"] = 1024 * (2 * d["FETCH_SIZE_KiB"] + d["WRITE_SIZE_KiB"])
+    if n_states is not None:  # model size of the profiled command (bench.py pmc_traffic)
+        for d in per.values():
+            d["n_states"] = n_states
     json.dump(per, open(os.path.join(out_dir, f"{tag}_summary.json"), "w"), indent=1)
     print(json.dumps(per, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else None)
