@@ -113,6 +113,15 @@ ITR_API int itr_viterbi(itr_model_t model, itr_plan_t plan, const uint16_t* d_ob
 ITR_API int itr_posterior(itr_model_t model, itr_plan_t plan, const uint16_t* d_obs,
                           double* d_post, void* stream);
 
+/* Packs the caller's per-block symbol arrays (the reference's V_lst: one int64 array per
+ * MAF block, read_data.py:94-117, consumed by optimizer.py:40-116, 241-262, 357-377) into
+ * the uint16 column array and int64 block offsets the sweeps take.  h_blocks[k] points at
+ * h_lens[k] int64 symbols; h_obs holds sum(h_lens), h_block_off n_blocks + 1 entries.
+ * A symbol outside [0, 625) fails with ITR_EDATA, naming the block and column
+ * (the reference's fancy index would raise IndexError).  Host memory only, multi-threaded. */
+ITR_API int itr_pack_symbols(const int64_t* const* h_blocks, const int64_t* h_lens,
+                             int64_t n_blocks, uint16_t* h_obs, int64_t* h_block_off);
+
 /* Host-buffer conveniences (synchronous; copy in, run, copy out). */
 ITR_API int itr_forward_loglik_host(itr_model_t model, itr_plan_t plan,
                                     const uint16_t* h_obs, double* h_loglik);

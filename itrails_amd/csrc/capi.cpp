@@ -8,7 +8,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/itrails_hip.h"
@@ -743,6 +745,59 @@ int itr_maf_copy(itr_maf_t h, uint16_t* obs, int64_t* block_off, int64_t* coords
 
 int itr_maf_close(itr_maf_t h) {
   delete h;
+  return 0;
+}
+
+// V_lst -> (uint16 columns, int64 offsets): the blocks are split into contiguous ranges of
+// about equal column count, one per thread; each thread converts and range-checks its own
+// blocks, and the first bad symbol (lowest block) is reported.
+int itr_pack_symbols(const int64_t* const* blocks, const int64_t* lens, int64_t n_blocks,
+                     uint16_t* obs, int64_t* block_off) {
+  if (n_blocks < 0 || !block_off || (n_blocks > 0 && !lens))
+    return fail(ITR_EINVAL, "bad pack arguments");
+  block_off[0] = 0;
+  for (int64_t k = 0; k < n_blocks; ++k) {
+    if (lens[k] < 0) return fail(ITR_EINVAL, "block %lld has negative length", (long long)k);
+    if (lens[k] > 0 && !blocks[k]) return fail(ITR_EINVAL, "block %lld is null", (long long)k);
+    block_off[k + 1] = block_off[k] + lens[k];
+  }
+  const int64_t total = block_off[n_blocks];
+  if (total == 0) return 0;
+  if (!obs) return fail(ITR_EINVAL, "null output");
+  const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, total >> 20));
+  std::vector<int64_t> bad(nt, -1), bad_col(nt, -1);
+  auto work = [&](int w) {
+    const int64_t lo_col = total * w / nt, hi_col = total * (w + 1) / nt;
+    // blocks whose first column falls in [lo_col, hi_col)
+    int64_t k = std::lower_bound(block_off, block_off + n_blocks, lo_col) - block_off;
+    for (; k < n_blocks && block_off[k] < hi_col; ++k) {
+      const int64_t* src = blocks[k];
+      uint16_t* dst = obs + block_off[k];
+      const int64_t len = lens[k];
+      int64_t ok = 1;
+      for (int64_t t = 0; t < len; ++t) {
+        const int64_t v = src[t];
+        ok &= (uint64_t)v < (uint64_t)ITR_NOBS;
+        dst[t] = (uint16_t)v;
+      }
+      if (!ok) {
+        int64_t t = 0;
+        while ((uint64_t)src[t] < (uint64_t)ITR_NOBS) ++t;
+        bad[w] = k;
+        bad_col[w] = t;
+        return;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int w = 1; w < nt; ++w) th.emplace_back(work, w);
+  work(0);
+  for (auto& t : th) t.join();
+  for (int w = 0; w < nt; ++w)
+    if (bad[w] >= 0)
+      return fail(ITR_EDATA, "observed symbol %lld (block %lld, column %lld) outside the "
+                  "625-letter alphabet", (long long)blocks[bad[w]][bad_col[w]],
+                  (long long)bad[w], (long long)bad_col[w]);
   return 0;
 }
 

@@ -64,7 +64,21 @@ class Model:
 def concat_blocks(V_lst: Sequence[np.ndarray]):
     """V_lst (list of int arrays of symbols, read_data.py:94-117) -> (uint16 obs, int64 off).
 
-    Symbols must be in [0, 625); the reference would raise IndexError on anything else."""
+    Symbols must be in [0, 625); the reference would raise IndexError on anything else.
+    Lists of int64 arrays (what read_data.py produces) are packed and range-checked by the
+    library in one threaded pass (itr_pack_symbols); anything else goes through NumPy."""
+    if V_lst and all(isinstance(v, np.ndarray) and v.dtype == np.int64 and v.ndim == 1
+                     and v.flags.c_contiguous for v in V_lst):
+        nb = len(V_lst)
+        lens = np.fromiter((v.shape[0] for v in V_lst), dtype=np.int64, count=nb)
+        ptrs = np.fromiter((v.ctypes.data for v in V_lst), dtype=np.uintp, count=nb)
+        obs = np.empty(int(lens.sum()), dtype=np.uint16)
+        off = np.empty(nb + 1, dtype=np.int64)
+        rc = lib().itr_pack_symbols(ptr(ptrs), ptr(lens), nb, ptr(obs), ptr(off))
+        if rc == _lib.ITR_EDATA:
+            raise IndexError(lib().itr_last_error().decode())
+        check(rc)
+        return obs, off
     lens = np.fromiter((len(v) for v in V_lst), dtype=np.int64, count=len(V_lst))
     off = np.zeros(len(V_lst) + 1, dtype=np.int64)
     np.cumsum(lens, out=off[1:])

@@ -38,3 +38,29 @@ def test_plan_rejects_decreasing_offsets():
     h = ctypes.c_void_p()
     assert L.itr_plan_create(off.ctypes.data, 2, ctypes.byref(h)) == _lib.ITR_EINVAL
     assert b"decrease" in L.itr_last_error()
+
+
+def test_pack_symbols_matches_numpy_and_rejects_bad_symbols():
+    """itr_pack_symbols (host only) == the NumPy concatenation; out-of-alphabet symbols
+    raise IndexError like the reference's fancy index; empty and ragged blocks."""
+    import numpy as np
+
+    from itrails_amd import hmm
+
+    rng = np.random.default_rng(5)
+    lens = [0, 1, 7, 0, 3000, 1 << 20, 2, 0]  # enough columns for several threads
+    V = [rng.integers(0, 625, n).astype(np.int64) for n in lens]
+    obs, off = hmm.concat_blocks(V)
+    assert obs.dtype == np.uint16 and off.dtype == np.int64
+    assert np.array_equal(off, np.concatenate([[0], np.cumsum(lens)]))
+    assert np.array_equal(obs, np.concatenate(V).astype(np.uint16))
+    # non-int64 input takes the NumPy path and agrees
+    o2, f2 = hmm.concat_blocks([v.astype(np.int32) for v in V])
+    assert np.array_equal(o2, obs) and np.array_equal(f2, off)
+    for bad in (625, -1, 1 << 40):
+        W = [v.copy() for v in V]
+        W[5][12345] = bad
+        with pytest.raises(IndexError, match="block 5, column 12345"):
+            hmm.concat_blocks(W)
+    e, eo = hmm.concat_blocks([np.zeros(0, dtype=np.int64)] * 3)
+    assert e.size == 0 and np.array_equal(eo, [0, 0, 0, 0])
