@@ -102,3 +102,21 @@ def test_full_size_posterior_rows(full):
     np.testing.assert_allclose(rows, ref, rtol=1e-8, atol=1e-300)
     del post
     torch.cuda.empty_cache()
+
+
+def test_full_size_posterior_host_copy(full):
+    """post_prob_wrapper from host blocks (itr_posterior_host: 5.6 GB of rows returned
+    through the chunked pinned-staging copy) equals the device-resident posterior bit for
+    bit, including the partial last chunk."""
+    import torch
+    obs, off = full["obs"], full["off"]
+    nb = int(np.searchsorted(off, 2_000_000))  # ~2 Mbp: 1.1 GB of rows, 9 chunks
+    V = [obs[off[k]:off[k + 1]].astype(np.int64) for k in range(nb)]
+    host = hmm.post_prob_wrapper(full["a"], full["b"], full["pi"], V)
+    plan = hmm.Plan(off[:nb + 1])
+    plan.reserve(full["a"].shape[0], posterior=True)
+    post = hmm.posterior_device(full["model"], plan, full["d_obs"][:off[nb]]).cpu().numpy()
+    assert len(host) == nb and all(h.shape == (len(v), 70) for h, v in zip(host, V))
+    assert np.array_equal(np.concatenate(host), post)
+    del post, host
+    torch.cuda.empty_cache()
