@@ -129,6 +129,10 @@ ITR_API int itr_viterbi_host(itr_model_t model, itr_plan_t plan, const uint16_t*
                              uint8_t* h_path);
 ITR_API int itr_posterior_host(itr_model_t model, itr_plan_t plan, const uint16_t* h_obs,
                                double* h_post);
+/* itr_posterior_host keeps two 128 MB pinned staging buffers (plus a stream and two events)
+ * per calling thread for large copy-outs, bound to the thread's current device and
+ * recreated when it changes; this frees the calling thread's set. */
+ITR_API int itr_release_staging(void);
 
 /* Timing hook for benchmarks: average device duration (ms) of the dominant kernel of the
  * last sweep issued on this thread, measured with HIP events on the sweep's stream. */
@@ -213,15 +217,18 @@ ITR_API int itr_maf_close(itr_maf_t maf);
 
 /* Viterbi segments CSV, byte-identical to workflow_viterbi.py:690-743 (csv excel dialect):
  * one row per run of equal states per block; with h_coords (per-column reference
- * positions, -9 = gap; NULL = block-relative positions) the reference's gap handling. */
+ * positions, -9 = gap; NULL = block-relative positions) the reference's gap handling.
+ * n_coords must equal the decoded column count h_block_off[n_blocks] (ITR_EINVAL
+ * otherwise; ignored when h_coords is NULL). */
 ITR_API int itr_write_viterbi_csv(const char* path, const uint8_t* h_states,
                                   const int64_t* h_block_off, int64_t n_blocks,
-                                  const int64_t* h_coords);
+                                  const int64_t* h_coords, int64_t n_coords);
 /* Posterior CSV, byte-identical to workflow_posterior.py:697-716: one row per column,
- * probabilities printed like Python repr(float); formatted by `threads` threads. */
+ * probabilities printed like Python repr(float); formatted by `threads` threads.
+ * n_coords as for itr_write_viterbi_csv. */
 ITR_API int itr_write_posterior_csv(const char* path, const double* h_post, int n_states,
                                     const int64_t* h_block_off, int64_t n_blocks,
-                                    const int64_t* h_coords, int threads);
+                                    const int64_t* h_coords, int64_t n_coords, int threads);
 /* Python repr(float) of x into out (cap >= 33 bytes suffices). */
 ITR_API int itr_format_float(double x, char* out, int cap);
 

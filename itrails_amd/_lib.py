@@ -43,6 +43,7 @@ _SIGNATURES = {
     "itr_forward_loglik_host": ([_P, _P, _P, _P], _I),
     "itr_viterbi_host": ([_P, _P, _P, _P], _I),
     "itr_posterior_host": ([_P, _P, _P, _P], _I),
+    "itr_release_staging": ([], _I),
     "itr_last_kernel_ms": ([ctypes.c_char_p, ctypes.POINTER(_D)], _I),
     "itr_expm_batched": ([_I, _I64, _P, _P, _P], _I),
     "itr_expm_batched_host": ([_I, _I64, _P, _P], _I),
@@ -56,8 +57,8 @@ _SIGNATURES = {
                        ctypes.POINTER(_I64)], _I),
     "itr_maf_copy": ([_P, _P, _P, _P, _P], _I),
     "itr_maf_close": ([_P], _I),
-    "itr_write_viterbi_csv": ([ctypes.c_char_p, _P, _P, _I64, _P], _I),
-    "itr_write_posterior_csv": ([ctypes.c_char_p, _P, _I, _P, _I64, _P, _I], _I),
+    "itr_write_viterbi_csv": ([ctypes.c_char_p, _P, _P, _I64, _P, _I64], _I),
+    "itr_write_posterior_csv": ([ctypes.c_char_p, _P, _I, _P, _I64, _P, _I64, _I], _I),
     "itr_format_float": ([_D, ctypes.c_char_p, _I], _I),
 }
 

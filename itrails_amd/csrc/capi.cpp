@@ -118,7 +118,9 @@ struct itr_model {
 struct itr_plan {
   int device = 0;
   int64_t nblocks = 0, total = 0;
+  int64_t ntiles = 0;            // Viterbi tile records: sum over blocks of ceil(T / 16)
   int64_t* d_off = nullptr;
+  int64_t* d_tile_off = nullptr;  // [nblocks+1] first tile record of every block
   int32_t* d_order = nullptr;
   int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
@@ -130,9 +132,9 @@ struct itr_plan {
   int32_t *d_tasks = nullptr, *d_split_blk = nullptr;
   double* d_svec = nullptr;
   int* d_sK = nullptr;
-  // workspace (grown on demand): forward rows (posterior) or omega rows (Viterbi), and the
-  // Viterbi stay flags
-  uint8_t* d_stay = nullptr;
+  // workspace (grown on demand): forward rows (posterior) or the Viterbi checkpoint rows,
+  // and the Viterbi stay-flag words
+  uint16_t* d_stay = nullptr;
   size_t stay_cap = 0;
   uint8_t* d_last = nullptr;
   double* d_alpha = nullptr;
@@ -158,18 +160,16 @@ int check_plan(itr_plan_t p) {
   return 0;
 }
 
-// row stride of the Viterbi stay flags: columns rounded up, plus slack so a 64-column
-// window never leaves the row
-int64_t stay_stride(int64_t total) { return ((total + 63) / 64) * 64 + 64; }
-
+// Workspace: Viterbi = one checkpoint row (f64) and one flag word (u16) per state per
+// 16-column tile record; posterior = the forward rows of every column.
 int reserve(itr_plan_t p, int n, bool vit, bool post) {
   const int xr = itr::sweep_row_stride(n, itr::MODE_VIT);
   const int xa = itr::sweep_row_stride(n, itr::MODE_BWD);
   if (xr < 0 || xa < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", n);
   size_t need_rows = 0;
   if (vit) {
-    need_rows = (size_t)p->total * xr;
-    const size_t need = (size_t)n * stay_stride(p->total);
+    need_rows = (size_t)std::max<int64_t>(p->ntiles, 1) * xr;
+    const size_t need = need_rows;
     if (need > p->stay_cap) {
       dev_free(p->d_stay);
       if (int e = dev_alloc(&p->d_stay, need)) return e;
@@ -195,6 +195,7 @@ itr::SweepArgs base_args(itr_model_t m, itr_plan_t p, const uint16_t* obs) {
   a.sink = p->d_sink;
   a.obs = obs;
   a.prio_len = p->prio_len;
+  a.tile_off = p->d_tile_off;
   return a;
 }
 
@@ -210,10 +211,10 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname) {
   if (grid > a.nblocks) grid = a.nblocks;
   if (grid <= 0) return 0;
   HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
+#ifdef ITR_DIAG
   if (getenv("ITR_VERBOSE"))
     fprintf(stderr, "[itr] %s: n=%d cfg=%d block=%d lds=%zu per_cu=%d grid=%lld\n", tname, a.n,
             g.iq, g.block, g.lds, g.per_cu, (long long)grid);
-#ifdef ITR_DIAG
   if (!g_diag) HIP_TRY(hipMalloc(&g_diag, 16 * sizeof(uint64_t)));
   HIP_TRY(hipMemsetAsync(g_diag, 0, 16 * sizeof(uint64_t), st));
   a.diag = g_diag;
@@ -319,6 +320,10 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   (void)hipGetDevice(&p->device);
   p->nblocks = nblocks;
   p->total = h_off[nblocks];
+  std::vector<int64_t> tile_off(nblocks + 1, 0);
+  for (int64_t k = 0; k < nblocks; ++k)
+    tile_off[k + 1] = tile_off[k] + itr::vit_tiles(h_off[k + 1] - h_off[k]);
+  p->ntiles = tile_off[nblocks];
   // longest-first processing order (stable: equal lengths keep block order)
   std::vector<int32_t> order(nblocks);
   std::iota(order.begin(), order.end(), 0);
@@ -340,6 +345,8 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   std::vector<int32_t> tasks, split_blk;
   std::vector<int64_t> tlen;
   {
+    // ITR_SPLIT_FRAC (read once here, at plan creation): 0 disables the split (tests compare
+    // the split forward with the unsplit one)
     const char* fr = getenv("ITR_SPLIT_FRAC");
     const double frac = fr ? atof(fr) : 0.5;
     const int64_t tmax = nblocks ? h_off[order[0] + 1] - h_off[order[0]] : 0;
@@ -373,6 +380,7 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   if (!e) e = dev_alloc(&p->d_svec, (size_t)p->nsplit * 2 * 256);
   if (!e) e = dev_alloc(&p->d_sK, (size_t)p->nsplit * 2);
   if (!e) e = dev_alloc(&p->d_off, nblocks + 1);
+  if (!e) e = dev_alloc(&p->d_tile_off, nblocks + 1);
   if (!e) e = dev_alloc(&p->d_order, nblocks);
   if (!e) e = dev_alloc(&p->d_queue, 8);
   if (!e) e = dev_alloc(&p->d_sink, 64);
@@ -383,6 +391,7 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
       e = fail(ITR_EHIP, "plan upload failed");
   };
   up(p->d_off, h_off.data(), (nblocks + 1) * sizeof(int64_t));
+  up(p->d_tile_off, tile_off.data(), (nblocks + 1) * sizeof(int64_t));
   up(p->d_order, order.data(), nblocks * sizeof(int32_t));
   up(p->d_tasks, tasks.data(), tasks.size() * sizeof(int32_t));
   up(p->d_split_blk, split_blk.data(), split_blk.size() * sizeof(int32_t));
@@ -397,6 +406,7 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
 int itr_plan_destroy(itr_plan_t p) {
   if (!p) return 0;
   dev_free(p->d_off);
+  dev_free(p->d_tile_off);
   dev_free(p->d_order);
   dev_free(p->d_queue);
   dev_free(p->d_sink);
@@ -464,55 +474,25 @@ int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
   a.queue = p->d_queue + 2;  // own counter: may run concurrently with a forward sweep
   a.alpha = p->d_alpha;
   a.stay = p->d_stay;
-  a.fs = stay_stride(p->total);
   a.last_state = p->d_last;
-  const itr::SweepGeometry pg = itr::pair_geometry(m->n);
-  if (pg.iq >= 0 && p->nblocks >= 2) {
-    // the longest blocks (at least half as long as the longest, at most one per CU) run
-    // one per workgroup; every other block is paired with its neighbour in the
-    // longest-first order
-    const char* fr = getenv("ITR_PAIR_SINGLE_FRAC");
-    const double frac = fr ? atof(fr) : 0.5;
-    int64_t ns = 0;
-    const int64_t longest = p->sorted_len[0];
-    while (ns < p->nblocks && ns < cu_count() &&
-           (double)p->sorted_len[ns] >= frac * (double)longest && longest > 0)
-      ++ns;
-    int64_t grid = (int64_t)pg.per_cu * cu_count();
-    const int64_t work = ns + (p->nblocks - ns + 1) / 2;
-    if (grid > work) grid = work;
-    itr::SweepArgs ps = a;  // single-block part: order[0, ns)
-    ps.nblocks = ns;
-    ps.queue = p->d_queue + 3;
-    ps.nsingle_wg = (int)std::min<int64_t>(ns, grid);
-    a.order = p->d_order + ns;
-    a.nblocks = p->nblocks - ns;
-    HIP_TRY(hipMemsetAsync(p->d_queue + 2, 0, 2 * sizeof(int), st));
-    if (getenv("ITR_VERBOSE"))
-      fprintf(stderr, "[itr] viterbi pairs: n=%d w=%d lds=%zu per_cu=%d grid=%lld singles=%lld\n",
-              m->n, pg.iq, pg.lds, pg.per_cu, (long long)grid, (long long)ns);
-    Scope sc("viterbi", st);
-    HIP_TRY(itr::launch_vit_pairs(pg, (int)grid, a, ps, st));
-  } else {
-    if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
-  }
+  if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
   itr::TraceArgs ta{};
   ta.n = m->n;
   ta.xr = itr::sweep_row_stride(m->n, itr::MODE_VIT);
-  ta.fs = a.fs;
   ta.nblocks = p->nblocks;
   ta.off = p->d_off;
+  ta.tile_off = p->d_tile_off;
   ta.order = p->d_order;
   ta.queue = p->d_queue + 1;
   ta.obs = obs;
   ta.log_a = m->la;
   ta.log_e = m->LE;
-  ta.omega = p->d_alpha;
+  ta.ckpt = p->d_alpha;
   ta.stay = p->d_stay;
   ta.last_state = p->d_last;
   ta.path = path;
-  // one wave per block, 4 waves per workgroup
-  const int64_t grid = std::min<int64_t>((p->nblocks + 3) / 4, (int64_t)cu_count() * 8);
+  // one wave per block, 4 waves per workgroup (LDS: 4 x 16 recomputed rows)
+  const int64_t grid = std::min<int64_t>((p->nblocks + 3) / 4, (int64_t)cu_count() * 4);
   HIP_TRY(hipMemsetAsync(ta.queue, 0, sizeof(int), st));
   Scope sc("traceback", st);
   HIP_TRY(itr::launch_vit_traceback(ta, (int)grid, st));
@@ -552,21 +532,47 @@ struct DevBuf {
 // on their own stream while host threads copy the previous chunk out, so the PCIe transfer
 // overlaps the faulting copies and those run on several cores.
 constexpr size_t kStageBytes = size_t(128) << 20;
+// The calling thread's staging buffers, stream and events; they belong to one device and
+// are recreated when the thread's current device changes.  itr_release_staging() frees them.
+struct Staging {
+  int device = -1;
+  void* stage[2] = {nullptr, nullptr};
+  hipStream_t cs = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  void release() {
+    for (int i = 0; i < 2; ++i) {
+      if (stage[i]) (void)hipHostFree(stage[i]);
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
+      stage[i] = nullptr;
+      ev[i] = nullptr;
+    }
+    if (cs) (void)hipStreamDestroy(cs);
+    cs = nullptr;
+    device = -1;
+  }
+};
+thread_local Staging g_stage;
+
 int copy_out_large(void* dst, const void* src, size_t bytes) {
   if (bytes < 2 * kStageBytes) {
     HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return 0;
   }
-  static thread_local void* stage[2] = {nullptr, nullptr};
-  static thread_local hipStream_t cs = nullptr;
-  static thread_local hipEvent_t ev[2] = {nullptr, nullptr};
-  if (!cs) {
-    HIP_TRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  Staging& sg = g_stage;
+  if (sg.device != dev) {
+    sg.release();
+    HIP_TRY(hipStreamCreateWithFlags(&sg.cs, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
-      HIP_TRY(hipHostMalloc(&stage[i], kStageBytes, hipHostMallocDefault));
-      HIP_TRY(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+      HIP_TRY(hipHostMalloc(&sg.stage[i], kStageBytes, hipHostMallocDefault));
+      HIP_TRY(hipEventCreateWithFlags(&sg.ev[i], hipEventDisableTiming));
     }
+    sg.device = dev;
   }
+  void* const* stage = sg.stage;
+  hipStream_t cs = sg.cs;
+  hipEvent_t* ev = sg.ev;
   HIP_TRY(hipStreamSynchronize(nullptr));  // the sweep ran on the null stream
   const size_t nch = (bytes + kStageBytes - 1) / kStageBytes;
   auto issue = [&](size_t c) -> int {
@@ -636,6 +642,11 @@ int itr_posterior_host(itr_model_t m, itr_plan_t p, const uint16_t* h_obs, doubl
   HIP_TRY(hipMemcpy(o.p, h_obs, p->total * sizeof(uint16_t), hipMemcpyHostToDevice));
   if (int e = itr_posterior(m, p, (const uint16_t*)o.p, (double*)y.p, nullptr)) return e;
   return copy_out_large(h_post, y.p, bytes);
+}
+
+int itr_release_staging(void) {
+  g_stage.release();
+  return 0;
 }
 
 int itr_last_kernel_ms(const char* which, double* ms) {
@@ -858,10 +869,25 @@ int itr_format_float(double x, char* out, int cap) {
   return 0;
 }
 
+namespace {
+// per-column reference coordinates must cover exactly the decoded columns: the writers read
+// coords[c] for every column c
+int check_coords(const int64_t* block_off, int64_t n_blocks, const int64_t* coords,
+                 int64_t n_coords) {
+  if (!coords) return 0;
+  const int64_t total = n_blocks > 0 ? block_off[n_blocks] : 0;
+  if (n_coords != total)
+    return fail(ITR_EINVAL, "%lld reference coordinates for %lld decoded columns",
+                (long long)n_coords, (long long)total);
+  return 0;
+}
+}  // namespace
+
 int itr_write_viterbi_csv(const char* path, const uint8_t* states, const int64_t* block_off,
-                          int64_t n_blocks, const int64_t* coords) {
+                          int64_t n_blocks, const int64_t* coords, int64_t n_coords) {
   if (!path || (n_blocks > 0 && (!states || !block_off)) || n_blocks < 0)
     return fail(ITR_EINVAL, "bad arguments");
+  if (int e = check_coords(block_off, n_blocks, coords, n_coords)) return e;
   std::string err;
   if (itr::write_viterbi_csv(path, states, block_off, n_blocks, coords, &err))
     return fail(ITR_EINVAL, "%s", err.c_str());
@@ -870,9 +896,10 @@ int itr_write_viterbi_csv(const char* path, const uint8_t* states, const int64_t
 
 int itr_write_posterior_csv(const char* path, const double* post, int n_states,
                             const int64_t* block_off, int64_t n_blocks, const int64_t* coords,
-                            int threads) {
+                            int64_t n_coords, int threads) {
   if (!path || n_states < 0 || n_blocks < 0 || (n_blocks > 0 && (!post || !block_off)))
     return fail(ITR_EINVAL, "bad arguments");
+  if (int e = check_coords(block_off, n_blocks, coords, n_coords)) return e;
   std::string err;
   if (itr::write_posterior_csv(path, post, n_states, block_off, n_blocks, coords, threads, &err))
     return fail(ITR_EINVAL, "%s", err.c_str());

@@ -637,22 +637,28 @@ __device__ __forceinline__ void sweep_device(const SweepArgs& p) {
         //   yd = fl(z_j + c), yo = fl(max_{i != j} z_i + c), omega_t[j] = max(yd, yo)
         // is bit-identical to the reference's value.  yd > yo means j is the unique maximum,
         // so bp(t, j) = j for certain: that is the stay flag.  Otherwise (a switch, or a tie
-        // the first-max rule must break) the traceback recomputes bp(t, j) exactly from the
-        // stored omega rows.  Rows (stride XR) and flags (state-major, stride fs) are stored
-        // by the q == 0 lane of each real state.
+        // the first-max rule must break) the traceback recomputes bp(t, j) exactly.
+        // What is stored, per 16-column tile k of the block (tile record tk0 + k, row
+        // stride XR): the omega row of the tile's first column (a checkpoint the traceback
+        // recomputes the tile's later rows from) and one 16-bit word of stay flags per
+        // state (bit u = column 16k + u), written once per tile by the q == 0 lane of each
+        // real state.
+        static_assert(TE == VIT_TILE, "Viterbi checkpoints are one per staged tile");
+        const int64_t tk0 = p.tile_off[blk];
         const int o0 = ot.get(0);
         double x[RJN];
 #pragma unroll
         for (int r = 0; r < RJN; ++r) {
           x[r] = jv[r] ? p.init[o0 * n + jr[r]] : -INFINITY;
-          if (q == 0 && jv[r]) p.alpha[c0 * XR + jr[r]] = x[r];
+          if (q == 0 && jv[r]) p.alpha[tk0 * XR + jr[r]] = x[r];
         }
-        uint8_t* stay_row[RJN];
-#pragma unroll
-        for (int r = 0; r < RJN; ++r) stay_row[r] = p.stay + (int64_t)jr[r] * p.fs + c0;
         wait_vmem_all();
         STAMP(-1);
         for (int t0 = 0; t0 < T; t0 += TE) {
+          const int64_t rec = (tk0 + t0 / TE) * XR;  // this tile's checkpoint / flag record
+          uint32_t bits[RJN];
+#pragma unroll
+          for (int r = 0; r < RJN; ++r) bits[r] = 0;
 #pragma unroll
           for (int sub = 0; sub < TE; ++sub) {
             const int t = t0 + sub;
@@ -704,23 +710,23 @@ __device__ __forceinline__ void sweep_device(const SweepArgs& p) {
               STAMP(2);
               combine_max<QL>(zo);  // max over i != j, identical in the 8 lanes
               STAMP(3);
-              bool st[RJN];
 #pragma unroll
               for (int r = 0; r < RJN; ++r) {
                 const double yd = (x[r] + ldiag[r]) + ec[r];
                 const double yo = zo[r] + ec[r];
-                st[r] = yd > yo;
+                bits[r] |= (uint32_t)(yd > yo) << sub;
                 x[r] = fmax(yd, yo);
               }
               STAMP(4);
-              if (q == 0) {
+              if (sub == 0 && q == 0) {  // the tile's checkpoint row (t = t0 >= 16)
 #pragma unroll
-                for (int r = 0; r < RJN; ++r) {
-                  if (jv[r]) {
-                    p.alpha[(c0 + t) * XR + jr[r]] = x[r];
-                    stay_row[r][t] = (uint8_t)st[r];
-                  }
-                }
+                for (int r = 0; r < RJN; ++r)
+                  if (jv[r]) p.alpha[rec + jr[r]] = x[r];
+              }
+              if ((sub == TE - 1 || t == T - 1) && q == 0) {  // the tile's flag words
+#pragma unroll
+                for (int r = 0; r < RJN; ++r)
+                  if (jv[r]) p.stay[rec + jr[r]] = (uint16_t)bits[r];
               }
               STAMP(5);
             }
@@ -770,256 +776,32 @@ __global__ void __launch_bounds__(64 * WV, (Occ<QL, WV, RJN, IQ, MODE>::value))
 }
 
 // ---------------------------------------------------------------------------------------
-// Paired Viterbi sweep: two MAF blocks of similar length per workgroup (neighbours in the
-// longest-first order).  Both blocks use the same transition matrix, so every lane's IQ
-// slice of log a serves two max-plus chains (one per block) and the 8-lane combine becomes
-// a reduce-scatter: the first DPP stage (q <-> 7 - q) hands each lane the other block's
-// partial of its own "home" block (q < 4: the first block, q >= 4: the second), the two
-// quad stages finish the maximum, and everything after the combine — the diagonal /
-// emission tail, the stay flag, the omega row store, the next step's publish — runs once
-// per lane for one block instead of once per lane for every block.  Per column that is
-// about a quarter fewer VALU instructions than the single-block sweep.  The two blocks'
-// published vectors live in two LDS regions 256-B apart in bank phase, so the combined
-// read pattern is the single-block one.  Blocks shorter than the pair's longer one simply
-// stop storing; the longest blocks of the launch (p_single) run one per workgroup on the
-// single-block path first, because there the step latency, not the instruction count,
-// bounds the launch.
+// Viterbi traceback (optimizer.py:336-354) over the checkpoint rows and stay flags of
+// MODE_VIT.  One wave per block (longest first from a work counter).  Walking down from the
+// last column with the current state s, the path stays in s as long as stay(t, s) holds:
+// lane l reads s's flag word of tile k - l, so one load covers 1,024 columns, and the
+// highest clear bit of the highest tile with one is the next column u to resolve.  There
+// bp(u, s) is the reference's first argmax over i of (omega_{u-1}[i] + log a_is) +
+// log e_s(u) (lane i, +64, +128; first-max reduction).  omega_{u-1} is rebuilt from the
+// checkpoint of its tile by at most 15 steps of the Viterbi recursion into the wave's LDS
+// rows, each value max_i (omega[i] + log a_ij) + log e_j — bit-identical to the sweep's
+// max(yd, yo) because IEEE rounding is monotone — and kept for further switches in the
+// same tile.
 // ---------------------------------------------------------------------------------------
-template <int WV, int IQ>
-struct PairLds {
-  static constexpr int IQS = IQ + (IQ & 1);
-  static constexpr int XS = 8 * IQS;
-  static constexpr int XP = ((XS + 64 + 31) / 32) * 32;  // region stride: a 256-B multiple
-  static constexpr int XR = WV * 8;
-  static constexpr int TE = 16;
-  static constexpr size_t bytes = (size_t)4 * XP * 8 + (size_t)2 * 2 * TE * XR * 8 +
-                                  (size_t)128 * 8 + 40 * 4 + (size_t)2 * 2 * 64 * WV * 2;
-};
-
-template <int WV, int IQ>
-__device__ __forceinline__ void vit_pair_device(const SweepArgs& p) {
-  using L = PairLds<WV, IQ>;
-  constexpr int W = WV;
-  constexpr int TB = 64 * W;
-  constexpr int IQS = L::IQS, XS = L::XS, XP = L::XP, XR = L::XR, TE = L::TE;
-  constexpr int NCH = IQ >= 4 ? 2 : 1;  // chains per block (two blocks interleave already)
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int n = p.n;
-  const int tid = threadIdx.x;
-  const int w = uni(tid >> 6);
-  const int l = tid & 63;
-  const int q = l & 7;
-  const int jl = l >> 3;
-  const int hs = q >> 2;  // home position in the pair after the combine
-  const int j = w * 8 + jl;
-  const bool jv = j < n;
-
-  double* X = reinterpret_cast<double*>(smem);  // [2 pos][2 buf][XP]
-  double* EST = X + 4 * XP;                     // [2 pos][2][TE][XR]
-  double* RED = EST + 2 * 2 * TE * XR;          // [2 pos][64]
-  int* SBLK = reinterpret_cast<int*>(RED + 128);
-  int* REDI = SBLK + 8;                                     // [2 pos][16]
-  uint16_t* OBS = reinterpret_cast<uint16_t*>(REDI + 32);  // [2 pos][2][TB]
-
-  const bool pub = jv && (q & 3) == 0;
-  const int jx = pub ? (j / IQ) * IQS + j % IQ : XS + l;
-  double m[IQ];
-  const double ldiag = jv ? p.mat[(int64_t)j * n + j] : 0.0;
-#pragma unroll
-  for (int k = 0; k < IQ; ++k) {
-    const int i = q * IQ + k;
-    m[k] = (i < n && jv) ? p.mat[(int64_t)i * n + j] : 0.0;
-    if (i == j) m[k] = -INFINITY;
-  }
-  lds_barrier();  // the single-block phase may still be reading LDS
-  for (int i = tid; i < 4 * XP; i += TB) X[i] = -INFINITY;
-  lds_barrier();
-
-  RowStage<W, XR, TE> est0, est1;
-  const int npairs = (int)((p.nblocks + 1) / 2);
-  for (;;) {
-    if (tid == 0) SBLK[0] = atomicAdd(p.queue, 1);
-    lds_barrier();
-    const int pi = uni(SBLK[0]);
-    lds_barrier();
-    if (pi >= npairs) break;
-    const int b0 = uni(p.order[2 * pi]);
-    const bool has1 = 2 * pi + 1 < p.nblocks;
-    const int b1 = has1 ? uni(p.order[2 * pi + 1]) : b0;
-    const int64_t c00 = p.off[b0], c01 = p.off[b1];
-    const int T0 = uni((int)(p.off[b0 + 1] - c00));
-    const int T1 = has1 ? uni((int)(p.off[b1 + 1] - c01)) : 0;
-    const int T = max(T0, T1), Tmin = min(T0, T1);
-    if (T > 0) {
-      const int64_t ch = hs ? c01 : c00;  // this lane's home block
-      const int Th = hs ? T1 : T0;
-      ObsTiles ot0{OBS, p.obs + c00, T0, +1, TB, 0};
-      ObsTiles ot1{OBS + 2 * TB, p.obs + c01, T1, +1, TB, 0};
-      ot0.start(tid);
-      ot1.start(tid);
-      lds_barrier();
-      auto row0 = [&](int s) -> int64_t { return s < T0 ? (int64_t)ot0.get(s) : -1; };
-      auto row1 = [&](int s) -> int64_t { return s < T1 ? (int64_t)ot1.get(s) : -1; };
-      double* EST0 = EST;
-      double* EST1 = EST + 2 * TE * XR;
-      est0.issue(p.emit, n, n, tid, 0, row0);
-      est1.issue(p.emit, n, n, tid, 0, row1);
-      est0.commit(EST0, tid);
-      est1.commit(EST1, tid);
-      est0.issue(p.emit, n, n, tid, TE, row0);
-      est1.issue(p.emit, n, n, tid, TE, row1);
-      lds_barrier();
-      const double* ESTh = hs ? EST1 : EST0;
-      auto staged = [&](const double* base, int s) {
-        return base[((s / TE) & 1) * TE * XR + (s & (TE - 1)) * XR + j];
-      };
-      const int o0 = hs ? ot1.get(0) : ot0.get(0);
-      double x = (jv && Th > 0) ? p.init[o0 * n + j] : -INFINITY;
-      if (pub && Th > 0) p.alpha[ch * XR + j] = x;
-      uint8_t* srow = p.stay + (int64_t)j * p.fs + ch;
-      double xfin = x;  // the shorter block's last omega (column Tmin - 1)
-      wait_vmem_all();
-      for (int t0 = 0; t0 < T; t0 += TE) {
-#pragma unroll
-        for (int sub = 0; sub < TE; ++sub) {
-          const int t = t0 + sub;
-          if (t >= 1 && t < T) {
-            const int buf = sub & 1;  // t0 is even
-            double* Xh = X + (hs * 2 + buf) * XP;
-            const double* Xo = X + ((1 - hs) * 2 + buf) * XP;
-            Xh[jx] = x;
-            double ec = 0.0;
-            if (sub != 0) ec = staged(ESTh, t);
-            if (sub == 0) {
-              ot0.advance(t, tid);
-              ot1.advance(t, tid);
-              if (t >= TE) {
-                const int slot = (t / TE) & 1;
-                est0.commit(EST0 + slot * TE * XR, tid);
-                est1.commit(EST1 + slot * TE * XR, tid);
-              }
-            }
-            lds_barrier();
-            if (sub == 0) {
-              if (t >= TE) {
-                est0.issue(p.emit, n, n, tid, t + TE, row0);
-                est1.issue(p.emit, n, n, tid, t + TE, row1);
-              }
-              ec = staged(ESTh, t);
-            }
-            const double* xh = Xh + q * IQS;
-            const double* xo = Xo + q * IQS;
-            double bh[NCH], bo[NCH];
-#pragma unroll
-            for (int c = 0; c < NCH; ++c) {
-              bh[c] = xh[c] + m[c];
-              bo[c] = xo[c] + m[c];
-            }
-#pragma unroll
-            for (int k = NCH; k < IQ; ++k) {
-              bh[k % NCH] = fmax(bh[k % NCH], xh[k] + m[k]);
-              bo[k % NCH] = fmax(bo[k % NCH], xo[k] + m[k]);
-            }
-            double zh = bh[0], zo = bo[0];
-#pragma unroll
-            for (int c = 1; c < NCH; ++c) {
-              zh = fmax(zh, bh[c]);
-              zo = fmax(zo, bo[c]);
-            }
-            // reduce-scatter: lane q takes lane 7-q's partial of q's home block (which is
-            // 7-q's other block), then the two quad stages
-            zh = fmax(zh, dpp_f64<DPP_HM>(zo));
-            zh = fmax(zh, dpp_f64<DPP_Q1>(zh));
-            zh = fmax(zh, dpp_f64<DPP_Q2>(zh));
-            const double yd = (x + ldiag) + ec;
-            const double yo = zh + ec;
-            const bool st = yd > yo;
-            x = fmax(yd, yo);
-            if (pub && t < Th) {
-              p.alpha[(ch + t) * XR + j] = x;
-              srow[t] = (uint8_t)st;
-            }
-            if (t == Tmin - 1) xfin = x;
-          }
-        }
-      }
-      // last state of each block = first argmax of its last omega row (optimizer.py:346)
-#pragma unroll
-      for (int pos = 0; pos < 2; ++pos) {
-        const int Tp = pos ? T1 : T0;
-        double bv = (hs == pos && jv && Tp > 0) ? (Tp == T ? x : xfin) : -INFINITY;
-        int bj = (hs == pos && jv) ? j : 0x7fffffff;
-        wave_first_max(bv, bj);
-        if (l == 0) {
-          RED[pos * 64 + w] = bv;
-          REDI[pos * 16 + w] = bj;
-        }
-      }
-      lds_barrier();
-      if (tid < 2) {
-        const int pos = tid;
-        const int Tp = pos ? T1 : T0;
-        if (Tp > 0) {
-          double b = RED[pos * 64];
-          int a = REDI[pos * 16];
-          for (int v = 1; v < W; ++v) {
-            const double c = RED[pos * 64 + v];
-            const int ci = REDI[pos * 16 + v];
-            if (c > b || (c == b && ci < a)) {
-              b = c;
-              a = ci;
-            }
-          }
-          p.last_state[pos ? b1 : b0] = (uint8_t)a;
-        }
-      }
-    }
-    lds_barrier();
-  }
+// LDS hand-off between lanes of one wave (the region is private to the wave)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
-// the launch: workgroups [0, ps.nsingle_wg) first run the longest blocks one at a time,
-// then every workgroup works through the pairs
-template <int WV, int IQ>
-__global__ void __launch_bounds__(64 * WV, (Occ<8, WV, 1, IQ, MODE_VIT>::value))
-    vit_pair_kernel(SweepArgs p, SweepArgs ps) {
-  if ((int)blockIdx.x < ps.nsingle_wg) sweep_device<8, WV, 1, IQ, MODE_VIT>(ps);
-  vit_pair_device<WV, IQ>(p);
-}
-
-// ---------------------------------------------------------------------------------------
-// Viterbi traceback (optimizer.py:336-354) over the omega rows and stay flags of MODE_VIT.
-// One wave per block (longest first from a work counter).  Walking down from the last
-// column with the current state s, the path stays in s as long as stay(t, s) holds, so the
-// wave reads s's flag row 256 columns per round trip (four 64-column windows in flight,
-// lane l on column t - 64w - l), writes the run of s in one store per window, and stops at
-// the first column whose flag is clear.  There it evaluates the reference's expression
-// for every i — (omega_{t-1}[i] + log a_is) + log e_s(t), lane i (+64, +128) — and takes
-// the first i equal to omega_t[s] (ballot, lowest set bit): that is np.argmax's first
-// maximum, because omega_t[s] is by construction the maximum of exactly these values.
-// ---------------------------------------------------------------------------------------
 template <int G>  // state groups of 64 lanes: n <= 64 G
-__device__ __forceinline__ int vit_bp(const TraceArgs& p, int64_t c0, int t, int s, int l) {
-  const int64_t col = c0 + t;
-  const int sym = min((int)p.obs[col], 624);
-  const double le = p.log_e[(int64_t)sym * p.n + s];
-  const double M = p.omega[col * p.xr + s];
-  const double* row = p.omega + (col - 1) * p.xr;
-  int res = -1;
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const int i = l + 64 * g;
-    double y = -INFINITY;
-    if (i < p.n) y = (row[i] + p.log_a[(int64_t)i * p.n + s]) + le;
-    const uint64_t hit = __ballot(y == M);
-    if (res < 0 && hit) res = 64 * g + __builtin_ctzll(hit);
-  }
-  return res < 0 ? 0 : res;  // unreachable: omega_t[s] is one of the y
-}
-
-template <int G>
 __global__ void __launch_bounds__(256) vit_trace_kernel(TraceArgs p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int l = threadIdx.x & 63;
+  const int n = p.n;
+  // this wave's rows of one tile: row u = omega at column 16 * ctile + u
+  double* rows = reinterpret_cast<double*>(smem) + (size_t)(threadIdx.x >> 6) * VIT_TILE * n;
   for (;;) {
     int bi = 0;
     if (l == 0) bi = atomicAdd(p.queue, 1);
@@ -1029,35 +811,87 @@ __global__ void __launch_bounds__(256) vit_trace_kernel(TraceArgs p) {
     const int64_t c0 = p.off[blk];
     const int T = uni((int)(p.off[blk + 1] - c0));
     if (T <= 0) continue;  // no barrier in this kernel: a wave-uniform continue is safe
+    const int64_t tk0 = p.tile_off[blk];
     uint8_t* path = p.path + c0;
     int s = uni((int)p.last_state[blk]);
     if (l == 0) path[T - 1] = (uint8_t)s;
-    int t = T - 1;  // column whose state (s) is known
+    int t = T - 1;             // column whose state (s) is known
+    int ctile = -1, cupto = -1;  // LDS rows hold columns 16 ctile .. cupto
     while (t >= 1) {
-      const uint8_t* fr = p.stay + (int64_t)s * p.fs + c0;
-      int f[4];
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const int u = t - 64 * w - l;
-        f[w] = (u >= 1) ? (int)fr[u] : 1;
+      const int k = t >> 4;
+      const int kt = k - l;
+      const uint32_t w = kt >= 0 ? (uint32_t)p.stay[(tk0 + kt) * p.xr + s] : 0xFFFFu;
+      uint32_t mask = l == 0 ? (2u << (t & 15)) - 1u : 0xFFFFu;  // columns <= t only
+      if (kt == 0) mask &= ~1u;  // column 0 has no step
+      const uint32_t clear = ~w & mask;
+      const uint64_t hit = __ballot(clear != 0);
+      int u;  // highest column <= t with a clear flag (or the window's lowest column - 1)
+      if (hit) {
+        const int lf = __builtin_ctzll(hit);
+        const uint32_t cw = (uint32_t)__shfl((int)clear, lf);
+        u = 16 * (k - lf) + (31 - __builtin_clz(cw));
+      } else {
+        u = max(1, 16 * (k - 63)) - 1;
       }
-      const int tb = t;
+      for (int c = u + l; c < t; c += 64) path[c] = (uint8_t)s;  // columns u+1..t stay
+      t = u;
+      if (!hit) continue;
+      // column u: a switch or a tie; bp(u, s) from omega_{u-1}
+      const int cc = u - 1;
+      const int tt = cc >> 4;
+      if (tt != ctile || cc > cupto) {
+        int start = cupto + 1;
+        if (tt != ctile) {
+          const double* ck = p.ckpt + (tk0 + tt) * p.xr;
+          for (int j = l; j < n; j += 64) rows[j] = ck[j];
+          start = 16 * tt + 1;
+          ctile = tt;
+        }
+        wave_lds_sync();
+        for (int c = start; c <= cc; ++c) {
+          const int sym = min((int)p.obs[c0 + c], 624);
+          const double* prev = rows + (c - 1 - 16 * tt) * n;
+          double* cur = rows + (c - 16 * tt) * n;
+          const double* le = p.log_e + (int64_t)sym * n;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const int top = tb - 64 * w;
-        if (top < 1) break;
-        const uint64_t clear = __ballot(f[w] == 0 && top - l >= 1);
-        const int nvalid = min(64, top);
-        const int run = clear ? __builtin_ctzll(clear) : nvalid;  // stay columns on top
-        if (l < run) path[top - l - 1] = (uint8_t)s;
-        t = top - run;
-        if (clear) {  // column t: switch or tie, resolve exactly
-          s = uni(vit_bp<G>(p, c0, t, s, l));
-          if (l == 0) path[t - 1] = (uint8_t)s;
-          t -= 1;
-          break;  // the windows still in registers belong to the old state
+          for (int g = 0; g < G; ++g) {
+            const int j = l + 64 * g;
+            if (j < n) {
+              double m0 = -INFINITY, m1 = -INFINITY;
+              int i = 0;
+#pragma unroll 4
+              for (; i + 1 < n; i += 2) {
+                m0 = fmax(m0, prev[i] + p.log_a[(int64_t)i * n + j]);
+                m1 = fmax(m1, prev[i + 1] + p.log_a[(int64_t)(i + 1) * n + j]);
+              }
+              if (i < n) m0 = fmax(m0, prev[i] + p.log_a[(int64_t)i * n + j]);
+              cur[j] = fmax(m0, m1) + le[j];
+            }
+          }
+          wave_lds_sync();
+        }
+        cupto = max(cupto, cc);
+      }
+      const double* prow = rows + (cc - 16 * tt) * n;
+      const int sym = min((int)p.obs[c0 + u], 624);
+      const double le = p.log_e[(int64_t)sym * n + s];
+      double best = -INFINITY;
+      int bidx = l;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int i = l + 64 * g;
+        if (i < n) {
+          const double y = (prow[i] + p.log_a[(int64_t)i * n + s]) + le;
+          if (g == 0 || y > best) {
+            best = y;
+            bidx = i;
+          }
         }
       }
+      wave_first_max(best, bidx);
+      s = uni(bidx);
+      if (l == 0) path[u - 1] = (uint8_t)s;
+      t = u - 1;
     }
   }
 }
@@ -1081,7 +915,7 @@ static constexpr Cfg kCfgs[] = {
     // eight lanes per target, three targets per lane, W = ceil(N / 24) waves
     {8, 3, 3, 9}, {8, 6, 3, 17}};
 static constexpr int kNarrow = 7;  // entries 0..6
-static constexpr int kNumCfgs = (int)(sizeof kCfgs / sizeof kCfgs[0]);
+[[maybe_unused]] static constexpr int kNumCfgs = (int)(sizeof kCfgs / sizeof kCfgs[0]);
 
 static int cfg_xr(int c) { return (64 / kCfgs[c].ql) * kCfgs[c].w * kCfgs[c].rj; }
 static bool fits(int c, int n) { return cfg_xr(c) >= n && kCfgs[c].ql * kCfgs[c].iq >= n; }
@@ -1090,13 +924,15 @@ static bool fits(int c, int n) { return cfg_xr(c) >= n && kCfgs[c].ql * kCfgs[c]
 // sweep runs fastest on three waves with three targets per lane (configuration 20), the
 // posterior sweeps too, Viterbi on the one-target-per-lane kernel (9); other sizes below.
 static int pick_cfg(int n, int mode) {
-  // experiments: force a configuration (ITR_VIT_CFG: the Viterbi sweep only)
+#ifdef ITR_DIAG
+  // diagnostic/experiment build only: force a configuration (ITR_VIT_CFG: Viterbi only)
   const char* force = (mode == MODE_VIT && getenv("ITR_VIT_CFG")) ? getenv("ITR_VIT_CFG")
                                                                   : getenv("ITR_SWEEP_CFG");
   if (force) {
     const int c = atoi(force);
     if (c >= 0 && c < kNumCfgs && fits(c, n)) return c;
   }
+#endif
   // (posterior sweeps at N = 70 on configuration 20: 465 -> 496 M columns/s,
   // scripts/gpu_cfgsmall.sh)
   if (n > 64 && n <= 72) return mode == MODE_VIT ? 9 : 20;
@@ -1201,10 +1037,12 @@ SweepGeometry sweep_geometry(int n, int mode) {
   // the three-wave forward kernel: one workgroup per CU beyond the occupancy API's count
   // (measured on the (5,5) model, 10 Mbp: 6.0 vs 6.8 ms)
   if (g.iq == 20 && mode == MODE_FWD_LL) g.per_cu = occ + 1;
-  // experiments: resident workgroups per CU (ITR_VIT_PER_CU: the Viterbi sweep only)
+#ifdef ITR_DIAG
+  // diagnostic/experiment build only: resident workgroups per CU
   const char* pcu = (mode == MODE_VIT && getenv("ITR_VIT_PER_CU")) ? getenv("ITR_VIT_PER_CU")
                                                                    : getenv("ITR_PER_CU");
   if (pcu && atoi(pcu) > 0) g.per_cu = atoi(pcu);
+#endif
   return g;
 }
 
@@ -1217,57 +1055,6 @@ hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepA
 int sweep_row_stride(int n, int mode) {  // padded target states: row stride of bp / alpha
   const int c = pick_cfg(n, mode);
   return c < 0 ? -1 : cfg_xr(c);
-}
-
-// Paired Viterbi sweep configurations: (waves, sources per lane) by state count
-// Opt-in (ITR_VIT_PAIRS=1): measured on the (5,5) model the paired sweep needs 13 % fewer
-// VALU instructions per column but its step takes 1.8x as long, so at two workgroups per CU
-// it is 5 % slower than the single-block sweep.
-static int pair_cfg(int n) {
-  if (!getenv("ITR_VIT_PAIRS")) return -1;
-  if (n > 64 && n <= 72) return 9;
-  if (n > 32 && n <= 64) return 8;
-  if (n > 16 && n <= 32) return 4;
-  return -1;
-}
-
-SweepGeometry pair_geometry(int n) {
-  SweepGeometry g{};
-  g.iq = pair_cfg(n);
-  if (g.iq < 0) return g;
-  const int w = g.iq;
-  g.block = 64 * w;
-  const int single_cfg = w == 9 ? 9 : (w == 8 ? 8 : 7);
-  size_t pl = 0;
-  int occ = 0;
-  switch (w) {
-    case 9: pl = PairLds<9, 9>::bytes; break;
-    case 8: pl = PairLds<8, 8>::bytes; break;
-    case 4: pl = PairLds<4, 4>::bytes; break;
-  }
-  g.lds = std::max(pl, lds_bytes(single_cfg, MODE_VIT));
-  hipError_t e = hipSuccess;
-  switch (w) {
-    case 9: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vit_pair_kernel<9, 9>, 576, g.lds); break;
-    case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vit_pair_kernel<8, 8>, 512, g.lds); break;
-    case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vit_pair_kernel<4, 4>, 256, g.lds); break;
-  }
-  g.per_cu = (e == hipSuccess && occ > 0) ? occ : 1;
-  const char* pcu = getenv("ITR_PAIR_PER_CU");
-  if (pcu && atoi(pcu) > 0) g.per_cu = atoi(pcu);
-  g.xp = single_cfg;  // the single-block configuration (row stride = its XR = 8 w)
-  return g;
-}
-
-hipError_t launch_vit_pairs(const SweepGeometry& g, int grid, const SweepArgs& p,
-                            const SweepArgs& ps, hipStream_t st) {
-  switch (g.iq) {
-    case 9: hipLaunchKernelGGL((vit_pair_kernel<9, 9>), dim3(grid), dim3(576), g.lds, st, p, ps); break;
-    case 8: hipLaunchKernelGGL((vit_pair_kernel<8, 8>), dim3(grid), dim3(512), g.lds, st, p, ps); break;
-    case 4: hipLaunchKernelGGL((vit_pair_kernel<4, 4>), dim3(grid), dim3(256), g.lds, st, p, ps); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
 }
 
 // log P of each split block from its two halves (one wave per block)
@@ -1296,11 +1083,11 @@ hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* sp
 hipError_t launch_vit_traceback(const TraceArgs& a, int grid, hipStream_t st) {
   if (a.nblocks <= 0) return hipSuccess;
   const int g = (a.n + 63) / 64;
+  const size_t lds = (size_t)4 * VIT_TILE * a.n * sizeof(double);  // 4 waves' tile rows
   switch (g) {
-    case 1: hipLaunchKernelGGL(vit_trace_kernel<1>, dim3(grid), dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(vit_trace_kernel<2>, dim3(grid), dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL(vit_trace_kernel<3>, dim3(grid), dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL(vit_trace_kernel<4>, dim3(grid), dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL(vit_trace_kernel<1>, dim3(grid), dim3(256), lds, st, a); break;
+    case 2: hipLaunchKernelGGL(vit_trace_kernel<2>, dim3(grid), dim3(256), lds, st, a); break;
+    case 3: hipLaunchKernelGGL(vit_trace_kernel<3>, dim3(grid), dim3(256), lds, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

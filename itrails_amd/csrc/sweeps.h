@@ -8,6 +8,11 @@ namespace itr {
 
 enum SweepMode { MODE_FWD_LL = 0, MODE_FWD_STORE = 1, MODE_BWD = 2, MODE_VIT = 3 };
 
+// Viterbi columns per tile: one omega checkpoint row and one 16-bit stay-flag word per
+// state per tile of every block (tiles start at each block's first column)
+constexpr int VIT_TILE = 16;
+inline int64_t vit_tiles(int64_t T) { return (T + VIT_TILE - 1) / VIT_TILE; }
+
 struct SweepArgs {
   int n;                        // hidden states
   int xp;                       // padded length of the LDS state vectors
@@ -22,18 +27,17 @@ struct SweepArgs {
   const double* init;           // pi*E or log(pi*E), 625 x n
   double* loglik;               // [nblocks]                       (MODE_FWD_LL)
   double* alpha;                // [total x XR] rescaled forward rows (FWD_STORE out, BWD in);
-                                //   Viterbi: the omega rows (MODE_VIT out)
+                                //   Viterbi: [tiles x XR] checkpoint rows (MODE_VIT out)
   double* post;                 // [total x n] posteriors          (MODE_BWD)
   double* sink;                 // [64] write target of padded states (MODE_BWD)
-  uint8_t* stay;                // [n x fs] 1 where bp(t, j) == j is certain (MODE_VIT)
-  int64_t fs;                   // row stride of `stay` (>= total)
+  uint16_t* stay;               // [tiles x XR] bit u of (tile, j): bp(16 tile + u, j) == j
+                                //   is certain (MODE_VIT)
+  const int64_t* tile_off;      // [nblocks+1] first tile record of every block (MODE_VIT)
   uint8_t* last_state;          // [nblocks] argmax of the last column (MODE_VIT)
   int prio_len;                 // blocks at least this long run at raised wave priority
   const int32_t* tasks;         // MODE_FWD_LL: [nblocks x 3] {block, split, slot}, see capi.cpp
   double* svec;                 // MODE_FWD_LL: [nsplit x 2 x XR] vectors of split blocks
   int* sK;                      // MODE_FWD_LL: [nsplit x 2] their power-of-two exponents
-  int nsingle_wg;               // paired Viterbi launch: workgroups that first run the
-                                //   single-block sweep over the longest blocks
   uint64_t* diag;               // diagnostic build only: per-segment cycle sums
   int diag_wave;                // diagnostic build only: the wave that reports
 };
@@ -52,31 +56,26 @@ SweepGeometry sweep_geometry(int n, int mode);
 int sweep_row_stride(int n, int mode);
 hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepArgs& a,
                         hipStream_t st);
-// Paired Viterbi sweep (two blocks per workgroup; g.iq < 0: not available for this n)
-SweepGeometry pair_geometry(int n);
-// p: the paired blocks (order / nblocks of the pairs), ps: the single-block part
-hipError_t launch_vit_pairs(const SweepGeometry& g, int grid, const SweepArgs& p,
-                            const SweepArgs& ps, hipStream_t st);
 
 // log-likelihoods of the split blocks of a forward sweep
 hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,
                                     const double* svec, const int* sK, double* loglik,
                                     hipStream_t st);
 
-// Viterbi traceback over the omega rows and stay flags written by MODE_VIT
+// Viterbi traceback over the checkpoint rows and stay flags written by MODE_VIT
 struct TraceArgs {
   int n;                      // hidden states
-  int xr;                     // row stride of the omega rows
-  int64_t fs;                 // row stride of the stay flags
+  int xr;                     // row stride of the tile records
   int64_t nblocks;
   const int64_t* off;         // [nblocks+1]
+  const int64_t* tile_off;    // [nblocks+1]
   const int32_t* order;       // [nblocks] longest first
   int* queue;                 // work counter, zero at launch
   const uint16_t* obs;        // [total]
   const double* log_a;        // n x n
   const double* log_e;        // 625 x n
-  const double* omega;        // [total x xr]
-  const uint8_t* stay;        // [n x fs]
+  const double* ckpt;         // [tiles x xr] omega at each tile's first column
+  const uint16_t* stay;       // [tiles x xr] stay-flag words
   const uint8_t* last_state;  // [nblocks]
   uint8_t* path;              // [total]
 };

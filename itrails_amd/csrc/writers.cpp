@@ -224,13 +224,16 @@ int write_posterior_csv(const char* path, const double* post, int n_states, cons
                                       (int)std::thread::hardware_concurrency()));
   const int64_t chunk = 1 << 14;  // rows per formatting task
   // two rounds of per-thread buffers: the workers format round k + 1 while this thread
-  // writes round k, so the (serial) file writes overlap the (parallel) formatting
-  std::vector<std::string> cur(nt), nxt(nt);
-  auto launch = [&](int64_t r0, std::vector<std::string>& buf) {
+  // writes round k, so the (serial) file writes overlap the (parallel) formatting.  The
+  // rounds alternate by index; each worker gets its destination string by value before it
+  // starts, so nothing it touches is rebound while it runs.
+  std::vector<std::string> bufs[2] = {std::vector<std::string>(nt), std::vector<std::string>(nt)};
+  auto launch = [&](int64_t r0, int round) {
     std::vector<std::thread> th;
     for (int t = 0; t < nt; ++t) {
-      th.emplace_back([&, r0, t] {
-        std::string& s = buf[t];
+      std::string* dst = &bufs[round][t];
+      th.emplace_back([&, r0, t, dst] {
+        std::string& s = *dst;
         s.clear();
         const int64_t a = r0 + t * chunk, b = std::min(total, a + chunk);
         if (a >= b) return;
@@ -254,12 +257,12 @@ int write_posterior_csv(const char* path, const double* post, int n_states, cons
     return th;
   };
   const int64_t step = chunk * nt;
-  std::vector<std::thread> th = launch(0, cur);
-  for (int64_t r0 = 0; r0 < total; r0 += step) {
+  std::vector<std::thread> th = launch(0, 0);
+  int round = 0;
+  for (int64_t r0 = 0; r0 < total; r0 += step, round ^= 1) {
     for (auto& x : th) x.join();
-    th = r0 + step < total ? launch(r0 + step, nxt) : std::vector<std::thread>();
-    for (int t = 0; t < nt; ++t) fwrite(cur[t].data(), 1, cur[t].size(), fh.f);
-    std::swap(cur, nxt);
+    th = r0 + step < total ? launch(r0 + step, round ^ 1) : std::vector<std::thread>();
+    for (int t = 0; t < nt; ++t) fwrite(bufs[round][t].data(), 1, bufs[round][t].size(), fh.f);
   }
   for (auto& x : th) x.join();
   if (ferror(fh.f)) {

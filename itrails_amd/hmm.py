@@ -130,12 +130,40 @@ def _stream_handle():
 # ---------------------------------------------------------------------------------------
 # device layer (torch.cuda tensors)
 # ---------------------------------------------------------------------------------------
+# The caller guarantees symbol values < 625 (concat_blocks / the MAF reader check them);
+# the kernels clamp out-of-range symbols for memory safety only.
+def _check_obs(plan: Plan, d_obs):
+    import torch
+
+    if d_obs.dtype not in (torch.int16, torch.uint16):
+        raise TypeError(f"d_obs must be int16/uint16 symbols, got {d_obs.dtype}")
+    if not d_obs.is_cuda or not d_obs.is_contiguous():
+        raise ValueError("d_obs must be a contiguous device tensor")
+    if d_obs.device.index != torch.cuda.current_device():
+        raise ValueError(f"d_obs lives on {d_obs.device}, current device is "
+                         f"cuda:{torch.cuda.current_device()}")
+    if d_obs.numel() < plan.total:
+        raise ValueError(f"d_obs holds {d_obs.numel()} columns, the plan {plan.total}")
+
+
+def _out(out, shape, dtype, device):
+    import torch
+
+    if out is None:
+        return torch.empty(shape, dtype=dtype, device=device)
+    if out.dtype != dtype or tuple(out.shape) != tuple(shape) or out.device != device \
+            or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous {dtype} tensor of shape {tuple(shape)} "
+                         f"on {device}")
+    return out
+
+
 def forward_loglik_device(model: Model, plan: Plan, d_obs, out=None):
     """Per-block log-likelihoods (float64 [nblocks]) for int16/uint16 symbols on device."""
     import torch
 
-    if out is None:
-        out = torch.empty(plan.nblocks, dtype=torch.float64, device=d_obs.device)
+    _check_obs(plan, d_obs)
+    out = _out(out, (plan.nblocks,), torch.float64, d_obs.device)
     check(lib().itr_forward_loglik(model.handle, plan.handle, ptr(d_obs), ptr(out),
                                    _stream_handle()))
     return out
@@ -145,8 +173,8 @@ def viterbi_device(model: Model, plan: Plan, d_obs, out=None):
     """Viterbi state per column (uint8 [total])."""
     import torch
 
-    if out is None:
-        out = torch.empty(plan.total, dtype=torch.uint8, device=d_obs.device)
+    _check_obs(plan, d_obs)
+    out = _out(out, (plan.total,), torch.uint8, d_obs.device)
     check(lib().itr_viterbi(model.handle, plan.handle, ptr(d_obs), ptr(out), _stream_handle()))
     return out
 
@@ -155,8 +183,8 @@ def posterior_device(model: Model, plan: Plan, d_obs, out=None):
     """Posterior state probabilities (float64 [total, N])."""
     import torch
 
-    if out is None:
-        out = torch.empty((plan.total, model.n), dtype=torch.float64, device=d_obs.device)
+    _check_obs(plan, d_obs)
+    out = _out(out, (plan.total, model.n), torch.float64, d_obs.device)
     check(lib().itr_posterior(model.handle, plan.handle, ptr(d_obs), ptr(out),
                               _stream_handle()))
     return out

@@ -50,7 +50,8 @@ def write_viterbi_csv(output_file: str, viterbi_result, ref_coordinates=None,
             raise ValueError("reference coordinates do not match the decoded columns")
     check(lib().itr_write_viterbi_csv(str(output_file).encode(), states.ctypes.data,
                                       off.ctypes.data, len(off) - 1,
-                                      coords.ctypes.data if coords is not None else None))
+                                      coords.ctypes.data if coords is not None else None,
+                                      len(coords) if coords is not None else 0))
 
 
 def write_posterior_csv(output_file: str, posterior_results, ref_coordinates=None,
@@ -70,9 +71,14 @@ def write_posterior_csv(output_file: str, posterior_results, ref_coordinates=Non
         coords = ref_coordinates if isinstance(ref_coordinates, np.ndarray) else \
             _flat(ref_coordinates, np.int64)[0]
         coords = np.ascontiguousarray(coords, dtype=np.int64)
+        if len(coords) != len(post):
+            raise ValueError("reference coordinates do not match the decoded columns")
+    if len(post) != (int(off[-1]) if len(off) else 0):
+        raise ValueError("posterior rows do not match the block offsets")
     check(lib().itr_write_posterior_csv(str(output_file).encode(), post.ctypes.data, int(n),
                                         off.ctypes.data, len(off) - 1,
                                         coords.ctypes.data if coords is not None else None,
+                                        len(coords) if coords is not None else 0,
                                         int(threads)))
 
 

@@ -137,3 +137,21 @@ def test_device_layer_matches_host_layer(gpu):
     np.testing.assert_array_equal(path, g["path"])
     np.testing.assert_array_equal(post, hmm._posteriors(model, plan, g["obs"]))
     assert hmm.last_kernel_ms("viterbi") > 0
+
+
+@pytest.mark.parametrize("n", [5, 70, 133, 192])
+def test_viterbi_frequent_switches(gpu, n):
+    """Weakly sticky transitions and sharp emissions: the path switches every few columns,
+    so nearly every 16-column tile holds several clear stay flags and the traceback rebuilds
+    omega rows from the tile checkpoint and reuses them for later switches in the tile."""
+    rng = np.random.default_rng(40 + n)
+    a, b, pi = random_hmm(rng, n, stay=(0.2, 0.6))
+    b = rng.dirichlet(np.full(256, 0.05), size=n)
+    lengths = [1, 2, 15, 16, 17, 31, 32, 33, 1023, 1024, 1025, 3000] + \
+        list(rng.integers(1, 700, size=20))
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=n, p_n=0.01, p_gap=0.01)
+    t = build_tables(a, b, pi)
+    ref = O.viterbi(t, obs, off)
+    assert (np.diff(ref.astype(np.int64)) != 0).mean() > 0.1  # the regime under test
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    np.testing.assert_array_equal(hmm._paths(model, plan, obs), ref)

@@ -111,3 +111,27 @@ def test_parallel_scan_equals_sequential(tmp_path, monkeypatch):
             assert np.array_equal(a, b)
     ref = O.maf_parser(str(path), SP)
     assert [x.tolist() for x in M.maf_parser(str(path), SP)] == ref
+
+
+def test_duplicate_species_record_block(tmp_path):
+    """A block holding two records of one species (hg38.chr1 + hg38.chr5): maf_parser keeps
+    it (its dict has 4 keys, read_data.py:106-110) while parse_coordinates drops it (5
+    matching records, read_data.py:166-180), exactly like the reference.  The writers then
+    see fewer coordinates than decoded columns and must refuse instead of reading past the
+    coordinate array."""
+    from itrails_amd import writers as W
+
+    path = tmp_path / "dup.maf"
+    _write(path, [[(f"{s}.x", 0, "+", 9, "ACGT") for s in SP],
+                  [("hg38.chr1", 10, "+", 99, "ACG"), ("hg38.chr5", 20, "+", 99, "TTT")]
+                  + [(f"{s}.x", 0, "+", 9, "GGA") for s in SP[1:]]])
+    assert [g.tolist() for g in M.maf_parser(str(path), SP)] == O.maf_parser(str(path), SP)
+    assert M.parse_coordinates(str(path), SP, "hg38") == O.parse_coordinates(str(path), SP, "hg38")
+    obs, off, coords, _ = M.read_maf(str(path), SP, "hg38")
+    assert off.tolist() == [0, 4, 7] and len(coords) == 4
+    states = np.zeros(len(obs), dtype=np.uint8)
+    with pytest.raises(ValueError):
+        W.write_viterbi_csv(str(tmp_path / "v.csv"), states, ref_coordinates=coords, block_off=off)
+    with pytest.raises(ValueError):
+        W.write_posterior_csv(str(tmp_path / "p.csv"), np.full((len(obs), 3), 1 / 3),
+                              ref_coordinates=coords, block_off=off)
