@@ -1,23 +1,34 @@
 #!/usr/bin/env python3
-"""Benchmark: alignment columns/s for forward + Viterbi on a synthetic 3-species + outgroup
-alignment (BASELINE.json config 2: 5 + 5 intervals -> N = 70 hidden states, 10 Mbp per GPU).
+"""Benchmark: alignment columns/s for forward + Viterbi on synthetic 3-species + outgroup
+alignments sampled from the iTRAILS (5,5) HMM (N = 70 hidden states), plus the
+log-likelihood relative error against the CPU restatement of the reference (BASELINE.json).
 
-One step = the whole decoding hot path over the batch already resident in HBM:
-  forward log-likelihood of every MAF block (optimizer.py:145-188) + the log-likelihood
-  exchange across ranks (RCCL all-reduce, N > 1) + Viterbi with traceback of every block
-  (optimizer.py:305-354).
-The HMM is the reference's own (5,5) model build (tests/golden/model_kat_5_5.npz, produced by
-trans_emiss_calc with the KAT parameters of SURVEY 8c); columns are sampled from it
-(itrails_amd/synth.py), geometric block lengths with mean 2 kbp.
+Workloads (--workload; default `auto`):
+  chr10   BASELINE config 2: one 10 Mbp alignment (5,036 blocks, geometric mean 2 kbp) on one
+          GPU — the N = 1 headline.  At N > 1 every rank decodes its own 10 Mbp (weak).
+  chr100  BASELINE config 4: ONE fixed 100 Mbp alignment (~50,000 blocks) sharded over the
+          ranks with itrails_amd.distributed.shard_ranges (contiguous block ranges balanced by
+          columns): strong scaling, the union over ranks is the same alignment at every N.
+  auto    chr10 at N = 1, chr100 at N > 1.
+One step = the decoding hot path over the rank's columns already resident in HBM: forward
+log-likelihood of every block (optimizer.py:145-188), the log-likelihood exchange (one RCCL
+all-reduce of the per-block vector, N > 1; optimizer.py:40-65 is the reference's fan-out),
+Viterbi with traceback of every block (optimizer.py:305-354).
 
-Contract: python bench.py --gpus N --steps K --warmup W ; for N > 1 launched by
-torch.distributed.run, one rank per GPU; rank 0 prints ONE JSON line.
+Contract: python bench.py --gpus N --steps K --warmup W.  For N > 1 either launched by
+torch.distributed.run (RANK/WORLD_SIZE/MASTER_* in the environment) or, when WORLD_SIZE is
+unset, this script starts its own N rank processes (children, before any GPU call).
+Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
+import re
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,15 +37,13 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 (vector = matrix rate), AMD spec
-
+FP64_SPEC_TFLOPS = 78.6  # MI355X FP64 vector / matrix (AMD spec, FMA counted as 2 flop)
 
 # KAT parameters, internal units of the {t_1} case: times and N times mu,
 # r over mu (workflow_optimize.py:360-380)
 MU = 2e-8
 KAT = {"t_1": 240000.0 * MU, "t_2": 40000.0 * MU, "N_AB": 50000.0 * MU, "N_ABC": 50000.0 * MU,
        "t_upper": 745069.3855 * MU, "r": 1e-8 / MU}
-
 
 # the introgression model: the KAT set plus B/C admixture 20 kyr before
 # the first speciation, {t_1} case (t_B = t_C = t_1 - t_m, int_optimizer.py:504-520),
@@ -44,6 +53,9 @@ INT_KAT = {"t_1": 240000.0 * MU, "t_2": 40000.0 * MU, "N_AB": 50000.0 * MU,
            "r": 1e-8 / MU, "t_m": 20000.0 * MU, "m": 0.1}
 
 
+# ---------------------------------------------------------------------------------------
+# models
+# ---------------------------------------------------------------------------------------
 def load_model_intro(n_int: int):
     """The introgression HMM built on the device (model/intro.py) before the timed region."""
     from itrails_amd.config import derive_times_int
@@ -64,51 +76,204 @@ def load_model(n_int: int):
     f = os.path.join(ROOT, "tests", "golden", f"model_kat_{n_int}_{n_int}.npz")
     if os.path.exists(f):
         g = np.load(f)
-        return g["a"], g["b"], g["pi"], f"itrails ({n_int},{n_int}) KAT model"
-    # (7,7): the reference build does not finish here; this is the device
-    # model build's output for the KAT parameters (scripts/model_timing.py)
+        return g["a"], g["b"], g["pi"], f"itrails ({n_int},{n_int}) KAT model (reference build)"
+    # no reference output at this size: the device model build's output for the KAT
+    # parameters (scripts/model_timing.py)
     f = os.path.join(ROOT, "tests", "data", f"model_device_{n_int}_{n_int}.npz")
     if os.path.exists(f):
         g = np.load(f)
         return g["a"], g["b"], g["pi"], (f"itrails ({n_int},{n_int}) KAT model, built by the "
                                          "device model build")
-    # same state count, random HMM (only until the reference model fixture exists)
-    n = {5: 70, 7: 133}.get(n_int, 70)
-    g = np.load(os.path.join(ROOT, "tests", "golden", f"sweep_syn{n}.npz"))
-    return g["a"], g["b"], g["pi"], f"random N={n} HMM (sweep_syn{n} fixture)"
+    raise SystemExit(f"no ({n_int},{n_int}) model fixture")
 
 
+# ---------------------------------------------------------------------------------------
+# workloads
+# ---------------------------------------------------------------------------------------
+WORKLOADS = {"chr10": 10_000_000, "chr100": 100_000_000}
+
+
+def make_workload(kind, a, b, pi, rank, world, mean_block, mbp=None):
+    """-> dict(obs, off, lo, hi, nblocks, cols_total, cols_local, lengths, scaling)."""
+    from itrails_amd.distributed import shard_ranges
+    from itrails_amd.synth import block_lengths, sample_alignment, sample_alignment_range
+
+    cols = int(mbp * 1e6) if mbp else WORKLOADS[kind]
+    rng = np.random.default_rng(12345)
+    lengths = block_lengths(rng, cols, mean_block)
+    if kind == "chr100":
+        lo, hi = shard_ranges(lengths, world)[rank]
+        obs, off = sample_alignment_range(a, b, pi, lengths, lo, hi, seed=777)
+        return dict(obs=obs, off=off, lo=lo, hi=hi, nblocks=len(lengths), cols_total=cols,
+                    cols_local=int(off[-1]), lengths=lengths, scaling="strong")
+    # chr10: the same block layout on every rank, content per rank (weak scaling at N > 1)
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=777 + rank)
+    nb = len(lengths)
+    return dict(obs=obs, off=off, lo=rank * nb, hi=(rank + 1) * nb, nblocks=nb * world,
+                cols_total=cols * world, cols_local=cols, lengths=lengths, scaling="weak")
+
+
+# ---------------------------------------------------------------------------------------
+# self-launch of N ranks (when not started by torch.distributed.run)
+# ---------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int) -> int:
+    """Start n child processes of this script, one per GPU, with the torch.distributed
+    environment; this process touches no GPU and exits with the worst child status."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
+# ---------------------------------------------------------------------------------------
+# peaks and counters from profiles/
+# ---------------------------------------------------------------------------------------
+def valu_peaks():
+    """Chip-wide FP64 VALU rates measured by scripts/micro/valu_peak.hip (HIP events), the
+    best over 1-8 waves per SIMD: (fma TFLOP/s, add+max Tops/s, source)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*valu_peak*.txt")))
+    if not files:
+        return FP64_SPEC_TFLOPS, FP64_SPEC_TFLOPS / 2, "AMD spec (no measured peak)"
+    fma, am = 0.0, 0.0
+    for line in open(files[-1]):
+        m = re.match(r"(\S+)\s+waves/SIMD \d+:\s+\S+ ms\s+(\S+) T", line)
+        if m and m.group(1) == "fma":
+            fma = max(fma, float(m.group(2)))
+        elif m and m.group(1) == "add+max":
+            am = max(am, float(m.group(2)))
+    return fma, am, os.path.relpath(files[-1], ROOT)
+
+
+def pmc_traffic(n, mode, tag_hint=""):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
+    of this command (scripts/gpu_round.sh -> scripts/summarize_profile.py ->
+    profiles/*_summary.json: FETCH_SIZE + WRITE_SIZE from separate passes, raw)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")),
+                   key=os.path.getmtime)
+    for f in reversed(files):
+        d = json.load(open(f))
+        for name, v in d.items():
+            if name.startswith("void itr::sweep_kernel<") and \
+                    name.endswith(f", {mode}>(itr::SweepArgs)") and \
+                    v.get("n_states", 70) == n and "hbm_bytes_raw" in v:
+                return round(v["hbm_bytes_raw"]), (
+                    f"{os.path.basename(f)} ({name}): FETCH_SIZE+WRITE_SIZE per launch, raw")
+    return None, "no PMC summary under profiles/ for this kernel"
+
+
+# ---------------------------------------------------------------------------------------
+# CPU restatement: checker + baseline (oracle/, test infrastructure; never the product)
+# ---------------------------------------------------------------------------------------
+def host_threads():
+    """Threads of this job's CPU share: OMP_NUM_THREADS when the box sets it (16 per GPU on
+    the MI355X pool), else every core."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return env or (os.cpu_count() or 1)
+
+
+def oracle_check_fv(a, b, pi, obs, off, ll_dev, path_dev, threads):
+    """Forward log-likelihood + Viterbi of every block of this rank on the CPU restatement
+    (OpenMP over blocks): the relative error of the device log-likelihoods, the path
+    equality, and the wall time (the all-cores CPU baseline)."""
+    from itrails_amd.tables import build_tables
+    from oracle import hmm_oracle as O
+
+    O.set_threads(threads)
+    t = build_tables(a, b, pi)
+    t0 = time.perf_counter()
+    ll_ref = O.forward_loglik(t, obs, off)
+    path_ref = O.viterbi(t, obs, off)
+    dt = time.perf_counter() - t0
+    rel = np.abs(ll_dev - ll_ref) / np.abs(ll_ref)
+    acc_d = acc_r = 0.0
+    for x, y in zip(ll_dev.tolist(), ll_ref.tolist()):
+        acc_d += x
+        acc_r += y
+    return dict(max_rel=float(rel.max()) if len(rel) else 0.0,
+                total_rel=abs(acc_d - acc_r) / abs(acc_r) if acc_r else 0.0,
+                equal=bool(np.array_equal(path_dev, path_ref)),
+                mismatches=int((path_dev != path_ref).sum()), seconds=dt,
+                cols=int(off[-1]))
+
+
+def oracle_time(a, b, pi, obs, off, sample_cols, threads, posterior):
+    """CPU restatement on a bounded prefix: (columns, seconds)."""
+    from itrails_amd.tables import build_tables
+    from oracle import hmm_oracle as O
+
+    O.set_threads(threads)
+    nb = max(1, min(int(np.searchsorted(off, sample_cols)), len(off) - 1))
+    o2 = off[: nb + 1]
+    ob = obs[: o2[-1]]
+    t = build_tables(a, b, pi)
+    t0 = time.perf_counter()
+    if posterior:
+        O.posterior(t, ob, o2)
+    else:
+        O.forward_loglik(t, ob, o2)
+        O.viterbi(t, ob, o2)
+    return int(o2[-1]), time.perf_counter() - t0
+
+
+def oracle_check_post(a, b, pi, obs, off, post_dev_rows, nb, threads):
+    from itrails_amd.tables import build_tables
+    from oracle import hmm_oracle as O
+
+    O.set_threads(threads)
+    t = build_tables(a, b, pi)
+    o2 = off[: nb + 1]
+    t0 = time.perf_counter()
+    ref = O.posterior(t, obs[: o2[-1]], o2)
+    dt = time.perf_counter() - t0
+    ok = bool(np.allclose(post_dev_rows, ref, rtol=1e-8, atol=1e-300))
+    big = ref > 1e-200
+    rel = float(np.max(np.abs(post_dev_rows[big] - ref[big]) / ref[big])) if big.any() else 0.0
+    return dict(ok=ok, max_rel=rel, cols=int(o2[-1]), seconds=dt)
+
+
+# ---------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=["auto", "chr10", "chr100"], default="auto")
     ap.add_argument("--n-int", type=int, default=5)
     ap.add_argument("--mode", choices=["fv", "posterior", "optimize"], default="fv",
-                    help="fv: forward + Viterbi (BASELINE config 2, the default); posterior: "
-                         "posterior decoding (config 3, use --n-int 7); optimize: one "
-                         "itrails-optimize objective evaluation per step = device model "
+                    help="fv: forward + Viterbi (BASELINE configs 2 and 4, the default); "
+                         "posterior: posterior decoding (config 3, use --n-int 7); optimize: "
+                         "one itrails-optimize objective evaluation per step = device model "
                          "rebuild + forward log-likelihood of the resident columns (config 5)")
-    ap.add_argument("--model", choices=["itrails", "introgression"], default="itrails",
-                    help="itrails: the plain ILS model (BASELINE configs); introgression: "
-                         "the B/C admixture model of itrails-int-* (SURVEY 8(f) row 4), "
-                         "built on the device at startup")
-    ap.add_argument("--mbp", type=float, default=10.0, help="columns per GPU (Mbp)")
+    ap.add_argument("--model", choices=["itrails", "introgression"], default="itrails")
+    ap.add_argument("--mbp", type=float, default=None, help="override the workload size")
     ap.add_argument("--mean-block", type=float, default=2000.0)
-    ap.add_argument("--cpu-sample", type=int, default=10_000_000,
-                    help="columns of the bounded CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0,
-                    help="repeat the CPU-baseline sample until this much time has passed")
-    ap.add_argument("--check", action="store_true", help="verify against the CPU oracle")
+    ap.add_argument("--verify", type=int, default=1,
+                    help="1: check every block against the CPU restatement (log-likelihood "
+                         "relative error, Viterbi equality); its timing is the CPU baseline")
+    ap.add_argument("--cpu-1core-cols", type=int, default=300_000,
+                    help="columns of the 1-core CPU-baseline sample (0 = skip)")
     ap.add_argument("--host-path", type=int, default=1,
-                    help="1: also time the drop-in wrappers on host NumPy buffers (model "
-                         "upload, H2D, sweeps, D2H, float64 paths; reported beside value)")
-    ap.add_argument("--concurrent", type=int, default=0,
-                    help="1: forward sweep on a side stream beside the Viterbi sweep")
+                    help="1: also time the drop-in wrappers on host NumPy buffers (N = 1)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the exchange with several ranks on one GPU)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -116,8 +281,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -127,21 +292,26 @@ def main():
         else:
             dist.init_process_group("gloo")
     cdev = dev if args.backend == "nccl" else torch.device("cpu")  # collective tensors
+    seen_world = dist.get_world_size() if world > 1 else 1
+
+    def allreduce(x, op="sum"):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+                               "min": dist.ReduceOp.MIN}[op])
+        return float(t.item())
 
     from itrails_amd import hmm
-    from itrails_amd.synth import block_lengths, sample_alignment
 
     intro = args.model == "introgression"
     a, b, pi, model_name = load_model_intro(args.n_int) if intro else load_model(args.n_int)
     n = a.shape[0]
-    cols = int(args.mbp * 1e6)
-    # identical block-length layout on every rank (weak scaling: the same work per GPU, so
-    # the makespan is not set by one rank drawing a longer tail block); content differs
-    rng = np.random.default_rng(12345)
-    lengths = block_lengths(rng, cols, args.mean_block)
+    kind = args.workload if args.workload != "auto" else ("chr10" if world == 1 else "chr100")
     t0 = time.time()
-    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=777 + rank)
+    W = make_workload(kind, a, b, pi, rank, world, args.mean_block, args.mbp)
     gen_s = time.time() - t0
+    obs, off, lo = W["obs"], W["off"], W["lo"]
 
     model = hmm.Model(a, b, pi)
     plan = hmm.Plan(off)
@@ -152,24 +322,18 @@ def main():
     d_ll = torch.empty(plan.nblocks, dtype=torch.float64, device=dev)
     d_path = torch.empty(plan.total, dtype=torch.uint8, device=dev)
     d_post = torch.empty((plan.total, n), dtype=torch.float64, device=dev) if post_mode else None
-    nblk_global = plan.nblocks
-    if world > 1:
-        counts = torch.tensor([plan.nblocks], device=cdev)
-        allc = [torch.zeros_like(counts) for _ in range(world)]
-        dist.all_gather(allc, counts)
-        counts = [int(c.item()) for c in allc]
-        nblk_global = sum(counts)
-        first = sum(counts[:rank])
-        d_ll_global = torch.zeros(nblk_global, dtype=torch.float64, device=cdev)
+    d_ll_global = torch.zeros(W["nblocks"], dtype=torch.float64, device=cdev)
 
-    fwd_ms, vit_ms, tb_ms = [], [], []
-    # forward log-likelihood and Viterbi are independent sweeps over the same resident
-    # columns: the forward runs on a side stream beside the Viterbi sweep, so the two
-    # kernels share the CUs and the long blocks of one overlap the bulk of the other
-    side = torch.cuda.Stream(device=dev) if args.concurrent else None
-
-    build_ms = []
+    fwd_ms, vit_ms, tb_ms, build_ms = [], [], [], []
     eval_no = [0]
+
+    def exchange():
+        # each rank owns a disjoint slice of the global block vector: the all-reduce is an
+        # exact gather (x + 0 = x); the block-order host sum happens after the timed region
+        d_ll_global.zero_()
+        d_ll_global[lo:lo + plan.nblocks] = d_ll.to(cdev)
+        if world > 1:
+            dist.all_reduce(d_ll_global)
 
     def opt_step(timing=False):
         # one objective evaluation at a nearby parameter vector (the simplex moves every
@@ -190,16 +354,9 @@ def main():
         hmm.forward_loglik_device(m1, plan, d_obs, out=d_ll)
         if timing:
             fwd_ms.append(hmm.last_kernel_ms("forward"))
-            vit_ms.append(hmm.last_kernel_ms("forward"))
-            tb_ms.append(0.0)
-        v = d_ll
-        if world > 1:
-            d_ll_global.zero_()
-            d_ll_global[first:first + plan.nblocks] = d_ll.to(cdev)
-            dist.all_reduce(d_ll_global)
-            v = d_ll_global
+        exchange()
         acc = 0.0
-        for y in v.cpu().numpy().tolist():
+        for y in d_ll_global.cpu().numpy().tolist():
             acc += y
         m1.close()
         return acc
@@ -213,27 +370,12 @@ def main():
             if timing:
                 fwd_ms.append(hmm.last_kernel_ms("posterior_fwd"))
                 vit_ms.append(hmm.last_kernel_ms("posterior_bwd"))
-                tb_ms.append(0.0)
             return
-        cur = torch.cuda.current_stream(dev)
-        if side is not None and not timing:
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
-            hmm.viterbi_device(model, plan, d_obs, out=d_path)
-            cur.wait_stream(side)
-        else:
-            hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
+        hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
         if timing:
             fwd_ms.append(hmm.last_kernel_ms("forward"))
-        if world > 1:
-            # each rank owns a disjoint slice of the global block vector: the all-reduce is
-            # an exact gather (x + 0 = x), and the host sums in block order
-            d_ll_global.zero_()
-            d_ll_global[first:first + plan.nblocks] = d_ll.to(cdev)
-            dist.all_reduce(d_ll_global)
-        if side is None or timing:
-            hmm.viterbi_device(model, plan, d_obs, out=d_path)
+        exchange()
+        hmm.viterbi_device(model, plan, d_obs, out=d_path)
         if timing:
             vit_ms.append(hmm.last_kernel_ms("viterbi"))
             tb_ms.append(hmm.last_kernel_ms("traceback"))
@@ -251,27 +393,41 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device=cdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = allreduce(time.perf_counter() - t0, "max")
     # kernel durations (HIP events on the launch stream), separate instrumented passes
     for _ in range(max(1, min(args.steps, 3))):
         step(timing=True)
         torch.cuda.synchronize()
 
-    total_cols = cols * world
-    value = total_cols * args.steps / dt
-    ll_total = None
-    ll_host = (d_ll_global if world > 1 else d_ll).cpu().numpy()
+    ll_global = d_ll_global.cpu().numpy()
     acc = 0.0
-    for v in ll_host.tolist():
+    for v in ll_global.tolist():  # block order, like loglik_wrapper's `acc +=`
         acc += v
     ll_total = acc
 
-    # the drop-in call from host buffers, in a process state like the reference caller's:
-    # the resident benchmark buffers (posterior rows, plan workspaces) released first
+    # checks against the CPU restatement, every rank on its own blocks
+    threads = host_threads()
+    check = None
+    if args.verify and args.mode == "fv":
+        c = oracle_check_fv(a, b, pi, obs, off, d_ll.cpu().numpy(), d_path.cpu().numpy(), threads)
+        check = {"loglik_max_rel_err": allreduce(c["max_rel"], "max"),
+                 "loglik_total_rel_err": allreduce(c["total_rel"], "max"),
+                 "viterbi_equal": bool(allreduce(1.0 if c["equal"] else 0.0, "min")),
+                 "viterbi_mismatched_columns": int(allreduce(c["mismatches"], "sum")),
+                 "columns_checked": int(allreduce(c["cols"], "sum")),
+                 "reference": "oracle/hmm_oracle.c (CPU restatement of optimizer.py:145-354, "
+                              "pinned to the reference's golden vectors)"}
+    elif args.verify and post_mode:
+        nb = max(1, int(np.searchsorted(off, 1_000_000)))
+        rows = d_post[: int(off[nb])].cpu().numpy()
+        c = oracle_check_post(a, b, pi, obs, off, rows, nb, threads)
+        sums = float((d_post.sum(dim=1) - 1.0).abs().max())
+        check = {"posterior_allclose_1e-8": bool(allreduce(1.0 if c["ok"] else 0.0, "min")),
+                 "posterior_max_rel_err": allreduce(c["max_rel"], "max"),
+                 "columns_checked": int(allreduce(c["cols"], "sum")),
+                 "row_sum_max_abs_dev_all_columns": allreduce(sums, "max")}
+
+    # the drop-in call from host buffers (N = 1), resident benchmark buffers released first
     host = None
     if args.host_path and not opt_mode and world == 1:
         d_post = None
@@ -279,40 +435,60 @@ def main():
         torch.cuda.empty_cache()
         host = host_path_rate(hmm, a, b, pi, obs, off, post_mode)
 
-    result = None
     if rank == 0:
-        vit_avg = float(np.mean(vit_ms))
-        # Viterbi: one add + one max per (i, j) pair; backward: one FMA
-        ops_per_col = 2.0 * n * n
-        achieved = ops_per_col * cols / (vit_avg * 1e-3) / 1e12
-        traffic, traffic_note = pmc_traffic(n, {"fv": 3, "posterior": 2, "optimize": 0}[args.mode])
+        cols_total = W["cols_total"]
+        cols_local = W["cols_local"]
+        fma_peak, am_peak, peak_src = valu_peaks()
+        fwd_avg = float(np.mean(fwd_ms)) if fwd_ms else 0.0
+        vit_avg = float(np.mean(vit_ms)) if vit_ms else 0.0
+        tb_avg = float(np.mean(tb_ms)) if tb_ms else 0.0
+        pair_ops = 2.0 * n * n  # per column: N^2 FMA (forward / backward) or N^2 add + N^2 max
+        step_ms = dt / args.steps * 1e3
+        if args.mode == "fv":
+            dom, dom_ms, dom_peak, dom_mode = "sweep_kernel<VIT> (Viterbi max-plus)", vit_avg, \
+                am_peak, 3
+            ideal_ms = pair_ops * cols_local / (fma_peak * 1e12) * 1e3 + \
+                pair_ops * cols_local / (am_peak * 1e12) * 1e3
+        elif post_mode:
+            dom, dom_ms, dom_peak, dom_mode = "sweep_kernel<BWD> (backward + posterior)", vit_avg, \
+                fma_peak, 2
+            ideal_ms = 2 * pair_ops * cols_local / (fma_peak * 1e12) * 1e3
+        else:
+            dom, dom_ms, dom_peak, dom_mode = "sweep_kernel<FWD_LL> (forward)", fwd_avg, \
+                fma_peak, 0
+            ideal_ms = pair_ops * cols_local / (fma_peak * 1e12) * 1e3
+        achieved = pair_ops * cols_local / (dom_ms * 1e-3) / 1e12 if dom_ms else 0.0
+        traffic, traffic_note = pmc_traffic(n, dom_mode)
         cpu = None
-        if opt_mode and intro:
-            # the reference's introgression build, timed when its golden model was made in
-            # the build container (tests/golden/make_golden.py intmodel; 8 cores shared)
+        if opt_mode:
             f = os.path.join(ROOT, "tests", "golden",
-                             f"model_int_ikat_{args.n_int}_{args.n_int}.npz")
-            if os.path.exists(f):
+                             f"model_int_ikat_{args.n_int}_{args.n_int}.npz" if intro else
+                             f"model_kat_{args.n_int}_{args.n_int}.npz")
+            if os.path.exists(f) and "build_seconds" in np.load(f):
                 sec = float(np.load(f)["build_seconds"])
                 cpu = {"value": round(1.0 / sec, 6), "unit": "evaluations/s", "cores": 8,
                        "kind": "reference",
-                       "sample": f"trans_emiss_calc_introgression ({args.n_int},{args.n_int}) "
-                                 f"{sec:.0f} s in the build container, not re-timed on the "
-                                 "GPU box"}
-        elif opt_mode:
-            # the reference's own model build: 615 s per (5,5) evaluation on the 8-core
-            # survey container; it cannot run on the GPU box
-            cpu = {"value": round(1.0 / 615.0, 6), "unit": "evaluations/s", "cores": 8,
-                   "kind": "reference",
-                   "sample": "trans_emiss_calc (5,5) measured once in the build container "
-                             "(BASELINE.md 2), not re-timed on the GPU box"}
-        elif args.cpu_sample > 0:
-            cpu = cpu_baseline(a, b, pi, obs, off, args.cpu_sample, args.cpu_seconds,
-                               post_mode)
-        check = None
-        if args.check and args.mode == "fv":
-            check = verify(a, b, pi, obs, off, ll_host if world == 1 else d_ll.cpu().numpy(),
-                           d_path.cpu().numpy())
+                       "sample": f"the reference's model build ({args.n_int},{args.n_int}) took "
+                                 f"{sec:.0f} s in the 8-core build container "
+                                 "(tests/golden/make_golden.py), not re-timed on the GPU box"}
+        elif world == 1:
+            # all cores of this job's share: the verification pass over the whole workload
+            # (fv) or the posterior check sample; 1 core: a bounded prefix
+            if check is not None:
+                ccols, csec = c["cols"], c["seconds"]
+            else:
+                ccols, csec = oracle_time(a, b, pi, obs, off, 2_000_000, threads, post_mode)
+            one = None
+            if args.cpu_1core_cols > 0:
+                c1, s1 = oracle_time(a, b, pi, obs, off, args.cpu_1core_cols, 1, post_mode)
+                one = {"value": round(c1 / s1, 1), "cores": 1,
+                       "sample": f"first {c1} columns, {s1:.2f} s"}
+            cpu = {"value": round(ccols / csec, 1), "unit": "columns/s", "cores": threads,
+                   "host_cpu_count": os.cpu_count(), "kind": "port",
+                   "sample": f"{'posterior' if post_mode else 'forward + Viterbi'} over "
+                             f"{ccols} columns of this workload, {csec:.2f} s on {threads} "
+                             "threads (OMP_NUM_THREADS = this job's CPU share)",
+                   "one_core": one}
         metric = {"fv": "alignment columns/s (forward+Viterbi), 3sp+outgroup HMM",
                   "posterior": "alignment columns/s (posterior decoding), 3sp+outgroup HMM",
                   "optimize": "itrails-optimize objective evaluations/s (device model rebuild "
@@ -320,8 +496,7 @@ def main():
         if intro:
             metric = metric.replace("3sp+outgroup HMM", "3sp+outgroup introgression HMM") \
                 .replace("itrails-optimize", "itrails-int-optimize")
-        if opt_mode:
-            value = args.steps / dt
+        value = args.steps / dt if opt_mode else cols_total * args.steps / dt
         result = {
             "metric": metric,
             "value": round(value, 4 if opt_mode else 1),
@@ -329,51 +504,52 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "ms_per_step": round(step_ms, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": W["scaling"],
             "vs_baseline": None,
             "dtype": "f64",
-            "data": f"synthetic: columns sampled from the {model_name}, "
-                    "geometric blocks mean 2 kbp, 1% gaps + 0.5% N",
-            "config": {"workload": f"{args.mbp:g} Mbp/GPU, {n_int_label(args.n_int)}, " +
+            "data": f"synthetic: columns sampled from the {model_name}, geometric blocks mean "
+                    f"{args.mean_block:g} columns, 1% gaps + 0.5% N",
+            "config": {"workload": f"{kind}: {cols_total / 1e6:g} Mbp " +
+                                   ("alignment sharded over the ranks" if W["scaling"] == "strong"
+                                    else "per GPU") + f", {args.n_int}+{args.n_int} intervals, " +
                                    {"fv": "forward loglik + Viterbi traceback",
                                     "posterior": "posterior decoding",
                                     "optimize": "model rebuild + forward loglik per "
                                                 "evaluation"}[args.mode],
                        "hmm": model_name, "hidden_states": n,
-                       "columns_per_gpu": cols, "blocks_per_gpu": int(plan.nblocks),
-                       "longest_block": int(np.diff(off).max()),
-                       "parallelism": f"block-sharded x{world}"},
-            "roofline": {"kernel": {"fv": "sweep_kernel<VIT> (Viterbi max-plus)",
-                                    "posterior": "sweep_kernel<BWD> (backward + posterior)",
-                                    "optimize": "sweep_kernel<FWD_LL> (forward)"}[args.mode],
-                         "bound": "mfma",
-                         "pipe": ("FP64 VALU (add/max; FP64 vector rate = FP64 matrix rate on "
-                                  "MI355X)" if args.mode == "fv" else
-                                  "FP64 VALU FMA (FP64 vector rate = FP64 matrix rate on "
-                                  "MI355X)"),
-                         "achieved": round(achieved, 4), "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 5),
-                         # add and max are two VALU instructions per pair (no fused form):
-                         # the instruction ceiling is half the FMA-counted FLOP/s figure
-                         **({"peak_valu_instr": FP64_PEAK_TFLOPS / 2,
-                             "frac_valu_instr": round(achieved / (FP64_PEAK_TFLOPS / 2), 5)}
-                            if args.mode == "fv" else {}),
-                         "traffic": traffic,
-                         "traffic_note": traffic_note,
-                         "kernel_ms": round(vit_avg, 4),
-                         "forward_ms": round(float(np.mean(fwd_ms)), 4),
-                         "traceback_ms": round(float(np.mean(tb_ms)), 4),
-                         "algorithmic": f"{ops_per_col:.0f} FP64 ops/column x {cols} columns"},
+                       "columns_total": cols_total, "blocks_total": int(W["nblocks"]),
+                       "columns_rank0": cols_local, "blocks_rank0": int(plan.nblocks),
+                       "longest_block_rank0": int(np.diff(off).max()) if plan.nblocks else 0,
+                       "parallelism": f"block-sharded x{world}",
+                       "world_size_seen": seen_world,
+                       "backend": (dist.get_backend() if world > 1 else None)},
+            "roofline": {"kernel": dom, "bound": "valu",
+                         "pipe": "FP64 VALU (add+max pairs)" if args.mode == "fv" else
+                                 "FP64 VALU FMA",
+                         "achieved": round(achieved, 4), "peak": round(dom_peak, 3),
+                         "unit": "TFLOP/s", "frac": round(achieved / dom_peak, 5),
+                         "peak_source": peak_src,
+                         "peak_fma_tflops": round(fma_peak, 3),
+                         "peak_add_max_tops": round(am_peak, 3),
+                         "peak_spec_tflops": FP64_SPEC_TFLOPS,
+                         "traffic": traffic, "traffic_note": traffic_note,
+                         "kernel_ms": round(dom_ms, 4),
+                         "forward_ms": round(fwd_avg, 4),
+                         "viterbi_ms": round(vit_avg, 4) if args.mode == "fv" else None,
+                         "traceback_ms": round(tb_avg, 4) if args.mode == "fv" else None,
+                         "algorithmic": f"{pair_ops:.0f} FP64 ops/column per sweep x "
+                                        f"{cols_local} columns (rank 0)",
+                         "step_ideal_ms": round(ideal_ms, 4),
+                         "step_frac": round(ideal_ms / step_ms, 5) if not opt_mode else None},
             "cpu_baseline": cpu,
             **({"build_ms": round(float(np.mean(build_ms)), 1)} if opt_mode else {}),
             **({"host_path": host} if host is not None else {}),
-            "loglik_total": ll_total,
+            **(check or {}),
+            "loglik_total": ll_total if args.mode != "posterior" else None,
             "gen_seconds": round(gen_s, 2),
         }
-        if check is not None:
-            result["check"] = check
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()
@@ -404,78 +580,7 @@ def host_path_rate(hmm, a, b, pi, obs, off, post_mode, reps=2):
     calls = "post_prob_wrapper" if post_mode else "loglik_wrapper + viterbi_wrapper"
     return {"value": round(cols / t, 1), "unit": "columns/s", "ms": round(t * 1e3, 2),
             "note": f"{calls} on {len(V_lst)} host int64 blocks: model upload, H2D, sweeps, "
-                    "D2H and float64 outputs included (best of {reps})".replace("{reps}",
-                                                                               str(reps))}
-
-
-def n_int_label(k):
-    return f"{k}+{k} intervals"
-
-
-def pmc_traffic(n, mode=3):
-    """HBM bytes per Viterbi launch from the committed rocprofv3 PMC summary of this same
-    command (scripts/gpu_profile.sh -> scripts/summarize_profile.py -> profiles/*_summary.json:
-    FETCH_SIZE + WRITE_SIZE, separate passes).  None when no summary for this model size."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))
-    for f in reversed(files):
-        d = json.load(open(f))
-        for name, v in d.items():
-            if name.startswith("void itr::sweep_kernel<") and name.endswith(f", {mode}>(itr::SweepArgs)") \
-                    and v.get("n_states", 70) == n and "hbm_bytes_raw" in v:
-                return round(v["hbm_bytes_raw"]), (
-                    f"{os.path.basename(f)} ({name}): FETCH_SIZE+WRITE_SIZE per launch, raw; "
-                    "the Viterbi sweep writes the f64 omega rows (padded-state stride) and "
-                    "the uint8 stay flags, the posterior sweep the f64 posterior rows")
-    return None, "no PMC summary under profiles/"
-
-
-def cpu_baseline(a, b, pi, obs, off, sample_cols, min_seconds=10.0, posterior=False):
-    """The repo's C restatement of the reference sweeps (oracle/, OpenMP over blocks),
-    forward + Viterbi on a bounded prefix of this rank's blocks, repeated until min_seconds
-    have passed."""
-    from itrails_amd.tables import build_tables
-    from oracle import hmm_oracle as O
-
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
-    os.environ["OMP_NUM_THREADS"] = str(cores)
-    nb = int(np.searchsorted(off, sample_cols))
-    nb = max(1, min(nb, len(off) - 1))
-    o2 = off[: nb + 1]
-    ob = obs[: o2[-1]]
-    t = build_tables(a, b, pi)
-    O.lib()
-    t0 = time.perf_counter()
-    reps = 0
-    while True:
-        if posterior:
-            O.posterior(t, ob, o2)
-        else:
-            O.forward_loglik(t, ob, o2)
-            O.viterbi(t, ob, o2)
-        reps += 1
-        dt = time.perf_counter() - t0
-        if dt >= min_seconds or reps >= 20:
-            break
-    return {"value": round(float(o2[-1]) * reps / dt, 1), "unit": "columns/s", "cores": cores,
-            "kind": "port",
-            "sample": f"first {nb} blocks ({int(o2[-1])} columns) of the same workload, "
-                      f"{'posterior' if posterior else 'forward + Viterbi'}, {reps} pass(es), "
-                      f"{dt:.2f} s"}
-
-
-def verify(a, b, pi, obs, off, ll, path):
-    from itrails_amd.tables import build_tables
-    from oracle import hmm_oracle as O
-
-    nb = int(np.searchsorted(off, 300_000))
-    o2 = off[: nb + 1]
-    t = build_tables(a, b, pi)
-    ref_ll = O.forward_loglik(t, obs[: o2[-1]], o2)
-    ref_p = O.viterbi(t, obs[: o2[-1]], o2)
-    rel = float(np.max(np.abs(ll[:nb] - ref_ll) / np.abs(ref_ll)))
-    return {"blocks": nb, "loglik_max_rel_err": rel,
-            "viterbi_equal": bool((path[: o2[-1]] == ref_p).all())}
+                    f"D2H and float64 outputs included (best of {reps})"}
 
 
 if __name__ == "__main__":

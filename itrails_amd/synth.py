@@ -96,3 +96,25 @@ def sample_alignment(a, b, pi, lengths, seed: int = 0, p_n: float = 0.005,
     code5 = ((digits[:, 0] * 5 + digits[:, 1]) * 5 + digits[:, 2]) * 5 + digits[:, 3]
     obs = _code5_to_index()[code5]
     return obs.astype(np.uint16), off, hidden
+
+
+def sample_alignment_range(a, b, pi, lengths, lo: int, hi: int, seed: int = 0,
+                           chunk: int = 512, **kw):
+    """Blocks [lo, hi) of one large alignment whose content does not depend on how it is
+    split: blocks are generated in fixed chunks of `chunk` blocks, chunk c from the seed
+    (seed, c), so every rank of a sharded run can sample its own shard and the union over
+    ranks is the same alignment for every world size.  Returns (obs, off) of the range,
+    off relative to block lo."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    if hi <= lo:
+        return np.zeros(0, dtype=np.uint16), np.zeros(1, dtype=np.int64)
+    parts = []
+    for c in range(lo // chunk, (hi - 1) // chunk + 1):
+        c0, c1 = c * chunk, min((c + 1) * chunk, len(lengths))
+        obs, off, _ = sample_alignment(a, b, pi, lengths[c0:c1], seed=int(seed) * 1_000_003 + c,
+                                       **kw)
+        s0, s1 = max(lo, c0) - c0, min(hi, c1) - c0
+        parts.append(obs[off[s0]:off[s1]])
+    off = np.zeros(hi - lo + 1, dtype=np.int64)
+    np.cumsum(lengths[lo:hi], out=off[1:])
+    return np.concatenate(parts), off

@@ -211,3 +211,7 @@ void oracle_posterior(int n, const double* a, const double* emit, const double* 
     free(tmp);
   }
 }
+
+/* threads of the OpenMP loops above (the CPU-baseline legs time 1 core and the job's share) */
+#include <omp.h>
+void oracle_set_threads(int k) { omp_set_num_threads(k > 0 ? k : 1); }

@@ -33,10 +33,17 @@ def lib():
         L.oracle_forward_loglik.argtypes = [ctypes.c_int, P, P, P, P, P, ctypes.c_int64, P]
         L.oracle_viterbi.argtypes = [ctypes.c_int, P, P, P, P, P, ctypes.c_int64, P]
         L.oracle_posterior.argtypes = [ctypes.c_int, P, P, P, P, P, ctypes.c_int64, P]
-        for f in (L.oracle_forward_loglik, L.oracle_viterbi, L.oracle_posterior):
+        L.oracle_set_threads.argtypes = [ctypes.c_int]
+        for f in (L.oracle_forward_loglik, L.oracle_viterbi, L.oracle_posterior,
+                  L.oracle_set_threads):
             f.restype = None
         _lib = L
     return _lib
+
+
+def set_threads(k: int) -> None:
+    """OpenMP threads of the following calls."""
+    lib().oracle_set_threads(int(k))
 
 
 def _p(x):

@@ -101,3 +101,25 @@ def test_sharded_loglik_gloo_matches_block_order_sum(world):
     assert abs(tots[0] - acc) <= 1e-12 * abs(acc)
     ranges = sorted((lo, hi) for _, _, lo, hi in res)
     assert ranges[0][0] == 0 and ranges[-1][1] == len(g["off"]) - 1
+
+
+def test_sharded_sampling_independent_of_world_size():
+    """bench.py's strong-scaling workload: every rank samples only its own shard
+    (sample_alignment_range), and the union over ranks is the same alignment at every
+    world size."""
+    from itrails_amd.synth import block_lengths, sample_alignment_range
+    g = golden("sweep_syn13.npz")
+    a, b, pi = g["a"], g["b"], g["pi"]
+    lengths = block_lengths(np.random.default_rng(1), 300_000, 400.0)
+    ref = None
+    for world in (1, 2, 3, 8):
+        parts = []
+        for lo, hi in shard_ranges(lengths, world):
+            obs, off = sample_alignment_range(a, b, pi, lengths, lo, hi, seed=5, chunk=64)
+            assert off[-1] == len(obs) == lengths[lo:hi].sum()
+            parts.append(obs)
+        allobs = np.concatenate(parts)
+        if ref is None:
+            ref = allobs
+        assert np.array_equal(allobs, ref)
+    assert len(ref) == 300_000
