@@ -130,6 +130,11 @@ struct itr_plan {
   // split blocks' scratch
   int64_t ntasks = 0, nsplit = 0;
   int32_t *d_tasks = nullptr, *d_split_blk = nullptr;
+  // hybrid (matrix-core) sweeps: the nurg longest blocks as VALU tasks (utasks: forward
+  // log-likelihood tasks; the posterior sweeps take order[0, nurg)), the rest as groups of
+  // four blocks in longest-first order
+  int64_t nurg = 0, nutasks = 0, ngroups = 0;
+  int32_t *d_utasks = nullptr, *d_groups = nullptr;
   double* d_svec = nullptr;
   int* d_sK = nullptr;
   // workspace (grown on demand): forward rows (posterior) or the Viterbi checkpoint rows,
@@ -176,7 +181,11 @@ int reserve(itr_plan_t p, int n, bool vit, bool post) {
       p->stay_cap = need;
     }
   }
-  if (post) need_rows = std::max(need_rows, (size_t)p->total * xa);
+  if (post) {
+    const itr::MfmaGeometry g = itr::mfma_geometry(n, itr::MODE_BWD);
+    const int stride = g.cfg >= 0 ? std::max(xa, g.xr) : xa;
+    need_rows = std::max(need_rows, (size_t)p->total * stride);
+  }
   if (need_rows > p->alpha_cap) {
     dev_free(p->d_alpha);
     if (int e = dev_alloc(&p->d_alpha, need_rows)) return e;
@@ -227,6 +236,45 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname) {
   return 0;
 }
 
+// Hybrid sweep (mfma_sweeps.hip): the plan's urgent VALU tasks (v.tasks / v.order, v.nblocks)
+// then its matrix-core groups, in one persistent launch.  g from itr::mfma_geometry.
+int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const itr::MfmaGeometry& g,
+               hipStream_t st, const char* tname) {
+  itr::MfmaArgs a{};
+  a.n = m->n;
+  a.ngroups = p->ngroups;
+  a.groups = p->d_groups;
+  a.queue = p->d_queue + 4;
+  a.off = p->d_off;
+  a.obs = v.obs;
+  a.mat = m->a;
+  a.emit = m->E;
+  a.init = m->PIE;
+  a.loglik = v.loglik;
+  a.alpha = v.alpha;
+  a.astride = g.xr;
+  a.post = v.post;
+  a.prio_len = INT32_MAX;
+  v.queue = p->d_queue + 3;
+  v.prio_len = 0;  // every VALU task of the hybrid is a long block: raised wave priority
+  const int64_t work = v.nblocks + (p->ngroups + g.gb - 1) / g.gb;
+  int per_cu = g.per_cu;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_HYB_PER_CU")) per_cu = atoi(getenv("ITR_HYB_PER_CU"));
+#endif
+  int64_t grid = std::min<int64_t>((int64_t)per_cu * cu_count(), work);
+  if (grid <= 0) return 0;
+  HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
+#ifdef ITR_DIAG
+  if (getenv("ITR_VERBOSE"))
+    fprintf(stderr, "[itr] %s hybrid: n=%d cfg=%d block=%d per_cu=%d grid=%lld valu=%lld groups=%lld\n",
+            tname, a.n, g.cfg, g.block, g.per_cu, (long long)grid, (long long)v.nblocks,
+            (long long)p->ngroups);
+#endif
+  Scope sc(tname, st);
+  HIP_TRY(itr::launch_hybrid_sweep(mode, g, (int)grid, a, v, st));
+  return 0;
+}
 
 }  // namespace
 
@@ -341,21 +389,35 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   // workgroup steps it column by column), so blocks at least half as long as the longest
   // (and >= 512 columns) become two half-length tasks — forward over the first half,
   // textbook backward over the second — whose vectors fwd_split_combine_kernel joins.
-  // Tasks run longest first.
-  std::vector<int32_t> tasks, split_blk;
-  std::vector<int64_t> tlen;
-  {
-    // ITR_SPLIT_FRAC (read once here, at plan creation): 0 disables the split (tests compare
-    // the split forward with the unsplit one)
-    const char* fr = getenv("ITR_SPLIT_FRAC");
-    const double frac = fr ? atof(fr) : 0.5;
-    const int64_t tmax = nblocks ? h_off[order[0] + 1] - h_off[order[0]] : 0;
-    for (int64_t k = 0; k < nblocks; ++k) {
+  // Tasks run longest first.  Two task lists over the same split blocks (slots):
+  //   tasks   every block (the VALU-only sweep, state counts without a matrix-core form);
+  //   utasks  the `nurg` longest blocks only: the VALU part of the hybrid sweeps
+  //           (mfma_sweeps.hip), whose matrix-core groups take the remaining blocks.
+  const int64_t tmax = nblocks ? h_off[order[0] + 1] - h_off[order[0]] : 0;
+  std::vector<int32_t> split_blk;
+  // ITR_SPLIT_FRAC (read once here, at plan creation): 0 disables the split (tests compare
+  // the split forward with the unsplit one)
+  const char* fr = getenv("ITR_SPLIT_FRAC");
+  const double frac = fr ? atof(fr) : 0.5;
+  auto is_split = [&](int64_t T) {
+    return frac > 0 && T >= 512 && (double)T >= frac * (double)tmax;
+  };
+  std::vector<int32_t> slot_of(nblocks, -1);
+  for (int64_t k = 0; k < nblocks; ++k) {
+    const int32_t b = order[k];
+    if (is_split(h_off[b + 1] - h_off[b])) {
+      slot_of[b] = (int32_t)split_blk.size();
+      split_blk.push_back(b);
+    }
+  }
+  auto make_tasks = [&](int64_t count) {
+    std::vector<int32_t> tasks;
+    std::vector<int64_t> tlen;
+    for (int64_t k = 0; k < count; ++k) {
       const int32_t b = order[k];
       const int64_t T = h_off[b + 1] - h_off[b];
-      if (frac > 0 && T >= 512 && (double)T >= frac * (double)tmax) {
-        const int32_t m = (int32_t)(T / 2), slot = (int32_t)split_blk.size();
-        split_blk.push_back(b);
+      if (slot_of[b] >= 0) {
+        const int32_t m = (int32_t)(T / 2), slot = slot_of[b];
         tasks.insert(tasks.end(), {b, m, slot, b, -m, slot});
         tlen.push_back(m);
         tlen.push_back(T - m + 1);
@@ -370,12 +432,35 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
     std::vector<int32_t> sorted(tasks.size());
     for (size_t k = 0; k < idx.size(); ++k)
       for (int c = 0; c < 3; ++c) sorted[3 * k + c] = tasks[3 * idx[k] + c];
-    tasks.swap(sorted);
-  }
+    return sorted;
+  };
+  std::vector<int32_t> tasks = make_tasks(nblocks);
+  // The hybrid sweeps' urgent set: blocks at least a quarter as long as the longest (and
+  // every split block).  A matrix-core group steps four blocks in about twice the VALU
+  // step time, so the longest blocks stay on the lower-latency VALU path while the bulk
+  // goes through the matrix cores.
+  double ufrac = 0.25;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_URGENT_FRAC")) ufrac = atof(getenv("ITR_URGENT_FRAC"));
+#endif
+  int64_t nurg = 0;
+  while (nurg < nblocks && (slot_of[order[nurg]] >= 0 ||
+                            (double)(h_off[order[nurg] + 1] - h_off[order[nurg]]) >=
+                                std::max(512.0, ufrac * (double)tmax)))
+    ++nurg;
+  p->nurg = nurg;
+  std::vector<int32_t> utasks = make_tasks(nurg);
+  std::vector<int32_t> groups;
+  for (int64_t k = nurg; k < nblocks; k += 4)
+    for (int64_t r = 0; r < 4; ++r) groups.push_back(k + r < nblocks ? order[k + r] : -1);
   p->ntasks = (int64_t)tasks.size() / 3;
   p->nsplit = (int64_t)split_blk.size();
+  p->nutasks = (int64_t)utasks.size() / 3;
+  p->ngroups = (int64_t)groups.size() / 4;
   int e = 0;
   if (!e) e = dev_alloc(&p->d_tasks, tasks.size());
+  if (!e) e = dev_alloc(&p->d_utasks, utasks.size());
+  if (!e) e = dev_alloc(&p->d_groups, groups.size());
   if (!e) e = dev_alloc(&p->d_split_blk, split_blk.size());
   if (!e) e = dev_alloc(&p->d_svec, (size_t)p->nsplit * 2 * 256);
   if (!e) e = dev_alloc(&p->d_sK, (size_t)p->nsplit * 2);
@@ -394,6 +479,8 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   up(p->d_tile_off, tile_off.data(), (nblocks + 1) * sizeof(int64_t));
   up(p->d_order, order.data(), nblocks * sizeof(int32_t));
   up(p->d_tasks, tasks.data(), tasks.size() * sizeof(int32_t));
+  up(p->d_utasks, utasks.data(), utasks.size() * sizeof(int32_t));
+  up(p->d_groups, groups.data(), groups.size() * sizeof(int32_t));
   up(p->d_split_blk, split_blk.data(), split_blk.size() * sizeof(int32_t));
   if (e) {
     itr_plan_destroy(p);
@@ -412,6 +499,8 @@ int itr_plan_destroy(itr_plan_t p) {
   dev_free(p->d_sink);
   dev_free(p->d_stay);
   dev_free(p->d_tasks);
+  dev_free(p->d_utasks);
+  dev_free(p->d_groups);
   dev_free(p->d_split_blk);
   dev_free(p->d_svec);
   dev_free(p->d_sK);
@@ -452,10 +541,18 @@ int itr_forward_loglik(itr_model_t m, itr_plan_t p, const uint16_t* obs, double*
   a.sK = p->d_sK;
   if (!a.tasks || (p->nsplit > 0 && (!a.svec || !a.sK || !p->d_split_blk)))
     return fail(ITR_ESTATE, "forward task tables missing");
-  if (int e = run_sweep(itr::MODE_FWD_LL, a, st, "forward")) return e;
-  HIP_TRY(itr::launch_fwd_split_combine(m->n, itr::sweep_row_stride(m->n, itr::MODE_FWD_LL),
-                                        (int)p->nsplit, p->d_split_blk, p->d_svec, p->d_sK,
-                                        loglik, st));
+  const itr::MfmaGeometry g = itr::mfma_geometry(m->n, itr::MODE_FWD_LL);
+  int xr = itr::sweep_row_stride(m->n, itr::MODE_FWD_LL);
+  if (g.cfg >= 0 && p->ngroups > 0) {
+    a.tasks = p->d_utasks;
+    a.nblocks = p->nutasks;
+    xr = g.xr;
+    if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, st, "forward")) return e;
+  } else {
+    if (int e = run_sweep(itr::MODE_FWD_LL, a, st, "forward")) return e;
+  }
+  HIP_TRY(itr::launch_fwd_split_combine(m->n, xr, (int)p->nsplit, p->d_split_blk, p->d_svec,
+                                        p->d_sK, loglik, st));
   return 0;
 }
 
@@ -512,6 +609,15 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
   a.emit = m->E;
   a.init = m->PIE;
   a.alpha = p->d_alpha;
+  const itr::MfmaGeometry g = itr::mfma_geometry(m->n, itr::MODE_FWD_STORE);
+  if (g.cfg >= 0 && p->ngroups > 0) {
+    // forward rows at the hybrid's stride g.xr for every block (reserve() sized for it)
+    const itr::MfmaGeometry gb = itr::mfma_geometry(m->n, itr::MODE_BWD);
+    a.nblocks = p->nurg;  // the VALU part: order[0, nurg)
+    if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, st, "posterior_fwd")) return e;
+    a.post = post;
+    return run_hybrid(itr::MODE_BWD, m, p, a, gb, st, "posterior_bwd");
+  }
   if (int e = run_sweep(itr::MODE_FWD_STORE, a, st, "posterior_fwd")) return e;
   a.post = post;
   return run_sweep(itr::MODE_BWD, a, st, "posterior_bwd");

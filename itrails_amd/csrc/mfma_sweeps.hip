@@ -1,0 +1,456 @@
+// mfma_sweeps.hip — forward / backward+posterior sweeps of the iTRAILS HMM on the FP64
+// matrix cores of MI355X (gfx950, CDNA4), four MAF blocks advanced in lock-step.
+//
+// Why lock-step: one block's column step is a vector x matrix product (1 x N . N x N), a
+// 1/16-occupied MFMA tile.  v_mfma_f64_4x4x4_4b_f64 computes four independent 4x4x4
+// products per instruction; with the four rows = four HMM blocks of similar length, every
+// instruction advances 4 blocks x 16 target states x 4 source states, and a column step of
+// the group is NK = ceil(N/4) instructions per 16-target tile (probed layout
+// scripts/micro/mfma4_layout.hip):
+//   sub-product g = (lane >> 2) & 3;  A: row lane & 3, k lane >> 4;  B: column lane & 3,
+//   k lane >> 4;  D: row lane >> 4, column lane & 3.
+// Here: A row = block of the group (x_{t-1} replicated over g), k-lane kk = lane >> 4 takes
+// sources kk*NK + s at MFMA step s (one contiguous LDS run per lane), B column + 4g =
+// target within the wave's 16-target tile, so lane l ends a step holding x_t of block
+// r = l >> 4 at target j = 16 w + 4 g + (l & 3).  The lane's NK-slice of `a` lives in
+// VGPRs for the whole kernel.  One wave per tile (NT waves); GB groups per workgroup share
+// those registers (GB = 2: every wave runs two independent MFMA chains per step).
+//
+// Per step: MFMA chain (4 accumulators) -> x emission -> exact power-of-two rescale (every
+// TE steps, maxima through LDS) -> publish to LDS -> one LDS-only barrier.  Emission values
+// (and, backward, the stored forward rows) are gathered per lane from the L2-resident
+// tables one tile of TE columns ahead, symbols two tiles ahead, so the step never waits on
+// memory.  Blocks of a group end at different columns: each block's outputs stop at its own
+// length (its lanes keep stepping on a clamped symbol, finite and unused).
+//
+// Numerics as the VALU sweeps (hmm_sweeps.hip): probability domain with exact 2^k
+// rescaling — the reference's log-space recursion (optimizer.py:165-238) up to rounding
+// (observed ~1e-15 relative; the bar is 1e-8).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "sweeps.h"
+#include "valu_sweep.h"
+
+namespace itr {
+namespace {
+
+// reductions over the 16 lanes of a DPP row (= the 16 targets of one block in one wave):
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_ror:8
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_f64<0xB1>(v);
+  v += dpp_f64<0x4E>(v);
+  v += dpp_f64<0x141>(v);
+  return v + dpp_f64<0x128>(v);
+}
+__device__ __forceinline__ double row16_max(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));
+  v = fmax(v, dpp_f64<0x4E>(v));
+  v = fmax(v, dpp_f64<0x141>(v));
+  return fmax(v, dpp_f64<0x128>(v));
+}
+
+__device__ __forceinline__ double mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+// Occupancy the register budget is sized for: GB = 1 kernels keep two workgroups per CU
+// (N <= 96; the VALU tasks' matrix slice and staging set the budget), GB = 2 kernels one
+// (their waves carry two groups each)
+template <int NT, int NK, int GB, int MODE>
+struct MOcc {
+  static constexpr int wgs = GB == 1 ? (NK <= 24 ? 2 : 1) : 1;
+  static constexpr int value = wgs * ((NT + 3) / 4);  // waves per SIMD (busiest SIMD)
+};
+
+// LDS of one matrix-core task (carved from the kernel's dynamic LDS)
+template <int NT, int NK, int GB>
+struct MLds {
+  static constexpr int KP = 4 * NK;
+  static constexpr size_t x_off = 0;                                   // X[GB][2][4][KP]
+  static constexpr size_t rs_off = x_off + (size_t)GB * 2 * 4 * KP * 8;  // RS[GB][2][NT][4]
+  static constexpr size_t rm_off = rs_off + (size_t)GB * 2 * NT * 4 * 8; // RM[GB][NT][4]
+  static constexpr size_t kf_off = rm_off + (size_t)GB * NT * 4 * 8;     // KF[GB][4]
+  static constexpr size_t bytes = kf_off + (size_t)GB * 4 * 4;
+};
+
+// One task of the matrix-core sweep: the GB groups g0 .. g0+GB-1 of p.groups.
+template <int NT, int NK, int GB, int MODE>
+__device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem, int g0) {
+  constexpr int KP = 4 * NK;                  // padded source count
+  constexpr int TE = GB == 1 ? 4 : 2;         // columns per prefetch tile
+  static_assert(TE >= 2 && 8 % TE == 0, "rescale every 8 steps at tile starts");
+  constexpr int TB = 64 * NT;
+  using LD = MLds<NT, NK, GB>;
+  auto X = reinterpret_cast<double (*)[2][4][KP]>(smem + LD::x_off);    // published vectors
+  auto RS = reinterpret_cast<double (*)[2][NT][4]>(smem + LD::rs_off);  // row partial sums
+  auto RM = reinterpret_cast<double (*)[NT][4]>(smem + LD::rm_off);     // row maxima
+  auto KF = reinterpret_cast<int (*)[4]>(smem + LD::kf_off);
+
+  const int n = p.n;
+  const int tid = threadIdx.x;
+  const int w = uni(tid >> 6);
+  const int l = tid & 63;
+  const int r = l >> 4;                            // block row of the group
+  const int j = 16 * w + 4 * ((l >> 2) & 3) + (l & 3);  // target state
+  const int ra = l & 3, kk = l >> 4;               // A operand: block row, k-lane
+  const bool jv = j < n;
+  const bool row_leader = (l & 15) == 0;
+
+  double B[NK];  // this lane's slice of a: rows kk*NK + s, column j (per task: a few L2
+                 // loads against thousands of steps, and nothing live across tasks)
+#pragma unroll
+  for (int s = 0; s < NK; ++s) {
+    const int i = kk * NK + s;
+    B[s] = (i < n && jv) ? p.mat[(int64_t)i * n + j] : 0.0;
+  }
+  for (int i = tid; i < GB * 2 * 4 * KP; i += TB) (&X[0][0][0][0])[i] = 0.0;
+  lds_barrier();
+  {
+    // this lane's block in each of its groups, and the lock-step length
+    int T[GB], Tmax = 0;
+    int64_t c0[GB];
+    int blk[GB];
+#pragma unroll
+    for (int gb = 0; gb < GB; ++gb) {
+      const int gi = g0 + gb;
+      blk[gb] = gi < p.ngroups ? p.groups[4 * gi + r] : -1;
+      c0[gb] = blk[gb] >= 0 ? p.off[blk[gb]] : 0;
+      T[gb] = blk[gb] >= 0 ? (int)(p.off[blk[gb] + 1] - c0[gb]) : 0;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int b2 = gi < p.ngroups ? p.groups[4 * gi + rr] : -1;
+        const int T2 = b2 >= 0 ? (int)(p.off[b2 + 1] - p.off[b2]) : 0;
+        Tmax = max(Tmax, T2);
+      }
+    }
+    Tmax = uni(Tmax);
+    if (MODE == MODE_FWD_LL && Tmax == 0 && tid < 4 * GB) {  // only empty blocks: log 1 = 0
+      const int gi = g0 + (tid >> 2);
+      const int b2 = gi < p.ngroups ? p.groups[4 * gi + (tid & 3)] : -1;
+      if (b2 >= 0) p.loglik[b2] = 0.0;
+    }
+    if (Tmax > 0) {
+      const bool urgent = Tmax >= p.prio_len;
+      if (urgent) __builtin_amdgcn_s_setprio(2);
+      // symbol of column t of this lane's block, clamped into the block (forward: t; the
+      // backward sweep asks for T - 1 - s)
+      auto sym = [&](int gb, int t) -> int {
+        const int tc = min(max(t, 0), max(T[gb] - 1, 0));
+        return T[gb] > 0 ? min((int)p.obs[c0[gb] + tc], 624) : 0;
+      };
+      int snxt[GB][TE];
+      double enxt[GB][TE];
+
+      if constexpr (MODE == MODE_FWD_LL || MODE == MODE_FWD_STORE) {
+        // ---------------- forward: x_t = (x_{t-1} @ a) * e_t  (optimizer.py:181-187)
+        double x[GB], xfin[GB];
+        int K[GB], Kfin[GB];
+#pragma unroll
+        for (int gb = 0; gb < GB; ++gb) {
+          x[gb] = (T[gb] > 0 && jv) ? p.init[sym(gb, 0) * n + j] : 0.0;
+          if (jv) X[gb][0][r][j] = x[gb];
+          if (MODE == MODE_FWD_STORE && T[gb] > 0) p.alpha[c0[gb] * p.astride + j] = x[gb];
+          xfin[gb] = x[gb];
+          K[gb] = Kfin[gb] = 0;
+#pragma unroll
+          for (int u = 0; u < TE; ++u) {
+            enxt[gb][u] = jv ? p.emit[sym(gb, u) * n + j] : 0.0;
+            snxt[gb][u] = sym(gb, TE + u);
+          }
+        }
+        wait_vmem_all();
+        lds_barrier();
+        for (int t0 = 0; t0 < Tmax; t0 += TE) {
+          double ecur[GB][TE];
+#pragma unroll
+          for (int gb = 0; gb < GB; ++gb) {
+#pragma unroll
+            for (int u = 0; u < TE; ++u) ecur[gb][u] = enxt[gb][u];
+#pragma unroll
+            for (int u = 0; u < TE; ++u) {
+              enxt[gb][u] = jv ? p.emit[snxt[gb][u] * n + j] : 0.0;
+              snxt[gb][u] = sym(gb, t0 + 2 * TE + u);
+            }
+          }
+#pragma unroll
+          for (int sub = 0; sub < TE; ++sub) {
+            const int t = t0 + sub;
+            if (t >= 1 && t < Tmax) {
+              const int buf = (t - 1) & 1;
+              double y[GB];
+#pragma unroll
+              for (int gb = 0; gb < GB; ++gb) {
+                const double* xs = &X[gb][buf][ra][kk * NK];
+                double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+                for (int s = 0; s < NK; s += 4) {
+                  a0 = mfma4(xs[s], B[s], a0);
+                  if (s + 1 < NK) a1 = mfma4(xs[s + 1], B[s + 1], a1);
+                  if (s + 2 < NK) a2 = mfma4(xs[s + 2], B[s + 2], a2);
+                  if (s + 3 < NK) a3 = mfma4(xs[s + 3], B[s + 3], a3);
+                }
+                y[gb] = (a0 + a1) + (a2 + a3);
+              }
+#pragma unroll
+              for (int gb = 0; gb < GB; ++gb) {
+                double sc = 1.0;
+                if (sub == 1 && (t0 & 7) == 0 && t > 1) {  // maxima of x_{t-1} (t-1 = 0 mod 8)
+                  double M = RM[gb][0][r];
+#pragma unroll
+                  for (int v = 1; v < NT; ++v) M = fmax(M, RM[gb][v][r]);
+                  if (M > 0.0 && M < INFINITY) {
+                    const int e = ilogb(M);
+                    sc = ldexp(1.0, -e);
+                    K[gb] += e;
+                  }
+                }
+                x[gb] = (y[gb] * ecur[gb][sub]) * sc;
+                if constexpr (MODE == MODE_FWD_LL) {
+                  if (t == T[gb] - 1) {
+                    xfin[gb] = x[gb];
+                    Kfin[gb] = K[gb];
+                  }
+                } else {
+                  if (t < T[gb]) p.alpha[(c0[gb] + t) * p.astride + j] = x[gb];
+                }
+                if (jv) X[gb][buf ^ 1][r][j] = x[gb];
+                if (sub == 0 && (t0 & 7) == 0) {  // every 8th column: maxima for the rescale
+                  const double m = row16_max(x[gb]);
+                  if (row_leader) RM[gb][w][r] = m;
+                }
+              }
+              lds_barrier();
+            }
+          }
+        }
+        if constexpr (MODE == MODE_FWD_LL) {
+          // log P = log(sum_j x_j) + K ln 2   (optimizer.py:160-162)
+#pragma unroll
+          for (int gb = 0; gb < GB; ++gb) {
+            const double s = row16_sum(xfin[gb]);
+            if (row_leader) RS[gb][0][w][r] = s;
+            if (w == 0 && row_leader) KF[gb][r] = Kfin[gb];
+          }
+          lds_barrier();
+          if (tid < 4 * GB) {
+            const int gb = tid >> 2, rr = tid & 3;
+            const int gi = g0 + gb;
+            const int b2 = gi < p.ngroups ? p.groups[4 * gi + rr] : -1;
+            if (b2 >= 0) {
+              double S = 0.0;
+              for (int v = 0; v < NT; ++v) S += RS[gb][0][v][rr];
+              const int T2 = (int)(p.off[b2 + 1] - p.off[b2]);
+              p.loglik[b2] = T2 > 0 ? log(S) + (double)KF[gb][rr] * LN2 : 0.0;
+            }
+          }
+        }
+      } else {
+        // ---------------- backward + posterior (optimizer.py:191-238)
+        //   beta_{T-1} = 1;  beta_{t-1} = (beta_t * e_t) @ a   (vector @ a: the reference's form)
+        //   post_t = alpha_t * beta_t / sum_j(alpha_t * beta_t)
+        // Step s handles column t = T - 1 - s of every block of the group.
+        double bt[GB];
+        double anxt[GB][TE];
+        auto arow = [&](int gb, int s) -> double {  // stored forward row of column T-1-s
+          const int tc = max(T[gb] - 1 - s, 0);
+          return (T[gb] > 0 && jv) ? p.alpha[(c0[gb] + tc) * p.astride + j] : 0.0;
+        };
+#pragma unroll
+        for (int gb = 0; gb < GB; ++gb) {
+          bt[gb] = (T[gb] > 0 && jv) ? 1.0 : 0.0;
+#pragma unroll
+          for (int u = 0; u < TE; ++u) {
+            enxt[gb][u] = jv ? p.emit[sym(gb, T[gb] - 1 - u) * n + j] : 0.0;
+            anxt[gb][u] = arow(gb, u);
+            snxt[gb][u] = sym(gb, T[gb] - 1 - (TE + u));
+          }
+        }
+        wait_vmem_all();
+        for (int s0 = 0; s0 < Tmax; s0 += TE) {
+          double ecur[GB][TE], acur[GB][TE];
+#pragma unroll
+          for (int gb = 0; gb < GB; ++gb) {
+#pragma unroll
+            for (int u = 0; u < TE; ++u) {
+              ecur[gb][u] = enxt[gb][u];
+              acur[gb][u] = anxt[gb][u];
+            }
+#pragma unroll
+            for (int u = 0; u < TE; ++u) {
+              enxt[gb][u] = jv ? p.emit[snxt[gb][u] * n + j] : 0.0;
+              anxt[gb][u] = arow(gb, s0 + TE + u);
+              snxt[gb][u] = sym(gb, T[gb] - 1 - (s0 + 2 * TE + u));
+            }
+          }
+#pragma unroll
+          for (int sub = 0; sub < TE; ++sub) {
+            const int s = s0 + sub;
+            if (s < Tmax) {
+              const int buf = s & 1;
+              double qv[GB];
+#pragma unroll
+              for (int gb = 0; gb < GB; ++gb) {
+                qv[gb] = acur[gb][sub] * bt[gb];  // padded states: 0 * 0
+                const double v = bt[gb] * ecur[gb][sub];
+                const double ps = row16_sum(qv[gb]);
+                if (row_leader) RS[gb][buf][w][r] = ps;
+                if (sub == 0 && (s0 & 7) == 0) {
+                  const double m = row16_max(v);
+                  if (row_leader) RM[gb][w][r] = m;
+                }
+                if (jv) X[gb][buf][r][j] = v;
+              }
+              lds_barrier();
+#pragma unroll
+              for (int gb = 0; gb < GB; ++gb) {
+                double S = RS[gb][buf][0][r];
+#pragma unroll
+                for (int v = 1; v < NT; ++v) S += RS[gb][buf][v][r];
+                if (s < T[gb] && jv) p.post[(c0[gb] + (T[gb] - 1 - s)) * n + j] = qv[gb] / S;
+                double sc = 1.0;
+                if (sub == 0 && (s0 & 7) == 0) {
+                  double M = RM[gb][0][r];
+#pragma unroll
+                  for (int v = 1; v < NT; ++v) M = fmax(M, RM[gb][v][r]);
+                  if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
+                }
+                const double* xs = &X[gb][buf][ra][kk * NK];
+                double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+                for (int q = 0; q < NK; q += 4) {
+                  a0 = mfma4(xs[q], B[q], a0);
+                  if (q + 1 < NK) a1 = mfma4(xs[q + 1], B[q + 1], a1);
+                  if (q + 2 < NK) a2 = mfma4(xs[q + 2], B[q + 2], a2);
+                  if (q + 3 < NK) a3 = mfma4(xs[q + 3], B[q + 3], a3);
+                }
+                bt[gb] = ((a0 + a1) + (a2 + a3)) * sc;
+              }
+            }
+          }
+        }
+      }
+      if (urgent) __builtin_amdgcn_s_setprio(0);
+    }
+    lds_barrier();
+  }
+}
+
+// The hybrid persistent sweep: the longest blocks (p.urgent: VALU tasks of `v`, one block —
+// or half of a split block — per workgroup, lowest step latency) first, then the bulk as
+// matrix-core groups.  One launch, one workgroup shape: no co-residency assumption between
+// kernels is needed for the long blocks to start at once.
+template <int NT, int NK, int GB, int MODE, int VRJ, int VIQ>
+__global__ void __launch_bounds__(64 * NT, (MOcc<NT, NK, GB, MODE>::value))
+    hybrid_sweep_kernel(MfmaArgs p, SweepArgs v) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int qslot[2];
+  for (;;) {
+    if (threadIdx.x == 0) qslot[0] = atomicAdd(v.queue, 1);
+    lds_barrier();
+    const int bi = uni(qslot[0]);
+    lds_barrier();
+    if (bi >= v.nblocks) break;
+    sweep_task<8, NT, VRJ, VIQ, MODE>(v, smem, bi);
+  }
+  for (;;) {
+    if (threadIdx.x == 0) qslot[1] = atomicAdd(p.queue, GB);
+    lds_barrier();
+    const int g0 = uni(qslot[1]);
+    lds_barrier();
+    if (g0 >= p.ngroups) break;
+    mfma_task<NT, NK, GB, MODE>(p, smem, g0);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// configurations by state count: NT tiles of 16 targets, NK k-steps of 4 sources, GB groups
+// ---------------------------------------------------------------------------------------
+struct MCfg {
+  int nmin, nmax, nt, nk, gb, viq;  // viq: sources per lane of the VALU tasks (8 lanes)
+};
+constexpr MCfg kMCfgs[] = {
+    {33, 48, 3, 12, 1, 6}, {49, 64, 4, 16, 1, 8}, {65, 72, 5, 18, 1, 9}, {73, 80, 5, 20, 1, 10},
+    {81, 96, 6, 24, 1, 12}, {129, 136, 9, 34, 2, 17}, {137, 144, 9, 36, 2, 18}};
+
+template <int NT, int NK, int GB, int MODE, int VIQ>
+size_t lds_h() {
+  using V = ValuSweep<8, NT, 2, VIQ, MODE>;
+  return std::max(MLds<NT, NK, GB>::bytes, V::lds_bytes);
+}
+template <int NT, int NK, int GB, int MODE, int VIQ>
+hipError_t launch_h(const MfmaArgs& a, const SweepArgs& v, int grid, hipStream_t st) {
+  const size_t lds = lds_h<NT, NK, GB, MODE, VIQ>();
+  hipLaunchKernelGGL((hybrid_sweep_kernel<NT, NK, GB, MODE, 2, VIQ>), dim3(grid), dim3(64 * NT),
+                     lds, st, a, v);
+  return hipGetLastError();
+}
+template <int NT, int NK, int GB, int MODE, int VIQ>
+int occ_h() {
+  int nb = 0;
+  const size_t lds = lds_h<NT, NK, GB, MODE, VIQ>();
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &nb, hybrid_sweep_kernel<NT, NK, GB, MODE, 2, VIQ>, 64 * NT, lds) != hipSuccess)
+    return 1;
+  return nb > 0 ? nb : 1;
+}
+
+template <int MODE>
+hipError_t dispatch_m(int c, bool launch, const MfmaArgs* a, const SweepArgs* v, int grid,
+                      hipStream_t st, int* occ) {
+#define ITR_MCFG(C, NT, NK, GB, VIQ)                                        \
+  case C:                                                                   \
+    if (launch) return launch_h<NT, NK, GB, MODE, VIQ>(*a, *v, grid, st);   \
+    *occ = occ_h<NT, NK, GB, MODE, VIQ>();                                  \
+    return hipSuccess;
+  switch (c) {
+    ITR_MCFG(0, 3, 12, 1, 6)
+    ITR_MCFG(1, 4, 16, 1, 8)
+    ITR_MCFG(2, 5, 18, 1, 9)
+    ITR_MCFG(3, 5, 20, 1, 10)
+    ITR_MCFG(4, 6, 24, 1, 12)
+    ITR_MCFG(5, 9, 34, 2, 17)
+    ITR_MCFG(6, 9, 36, 2, 18)
+  }
+#undef ITR_MCFG
+  return hipErrorInvalidValue;
+}
+
+hipError_t dispatch_mode_m(int mode, int c, bool launch, const MfmaArgs* a, const SweepArgs* v,
+                           int grid, hipStream_t st, int* occ) {
+  switch (mode) {
+    case MODE_FWD_LL: return dispatch_m<MODE_FWD_LL>(c, launch, a, v, grid, st, occ);
+    case MODE_FWD_STORE: return dispatch_m<MODE_FWD_STORE>(c, launch, a, v, grid, st, occ);
+    case MODE_BWD: return dispatch_m<MODE_BWD>(c, launch, a, v, grid, st, occ);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+MfmaGeometry mfma_geometry(int n, int mode) {
+  MfmaGeometry g{};
+  g.cfg = -1;
+  if (mode == MODE_VIT) return g;  // max-plus: no matrix-core form
+  for (int c = 0; c < (int)(sizeof kMCfgs / sizeof kMCfgs[0]); ++c)
+    if (n >= kMCfgs[c].nmin && n <= kMCfgs[c].nmax) g.cfg = c;
+  if (g.cfg < 0) return g;
+  g.block = 64 * kMCfgs[g.cfg].nt;
+  g.xr = 16 * kMCfgs[g.cfg].nt;
+  g.gb = kMCfgs[g.cfg].gb;
+  int occ = 1;
+  (void)dispatch_mode_m(mode, g.cfg, false, nullptr, nullptr, 0, nullptr, &occ);
+  g.per_cu = occ;
+  return g;
+}
+
+hipError_t launch_hybrid_sweep(int mode, const MfmaGeometry& g, int grid, const MfmaArgs& a,
+                               const SweepArgs& v, hipStream_t st) {
+  int occ = 0;
+  return dispatch_mode_m(mode, g.cfg, true, &a, &v, grid, st, &occ);
+}
+
+}  // namespace itr

@@ -57,6 +57,37 @@ int sweep_row_stride(int n, int mode);
 hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepArgs& a,
                         hipStream_t st);
 
+// Matrix-core sweeps (mfma_sweeps.hip): groups of four blocks advanced in lock-step
+struct MfmaArgs {
+  int n;                        // hidden states
+  int64_t ngroups;
+  const int32_t* groups;        // [ngroups x 4] block ids, longest group first (-1: none)
+  int* queue;                   // work counter, zero at launch
+  const int64_t* off;           // [nblocks+1]
+  const uint16_t* obs;          // [total]
+  const double* mat;            // a, n x n
+  const double* emit;           // E, 625 x n
+  const double* init;           // pi*E, 625 x n
+  double* loglik;               // [nblocks]                  (MODE_FWD_LL)
+  double* alpha;                // forward rows, row stride astride (FWD_STORE out, BWD in)
+  int64_t astride;
+  double* post;                 // [total x n]                (MODE_BWD)
+  int prio_len;                 // groups at least this long run at raised wave priority
+};
+struct MfmaGeometry {
+  int cfg;      // configuration index (negative: no matrix-core form for this n / mode)
+  int block;    // threads per workgroup
+  int xr;       // padded targets (row stride of stored forward rows >= xr)
+  int gb;       // groups per workgroup
+  int per_cu;   // resident workgroups per CU (occupancy API)
+};
+MfmaGeometry mfma_geometry(int n, int mode);
+// one launch: the VALU tasks of `v` (v.tasks / v.order, v.nblocks of them: the longest
+// blocks, on the VALU configuration {8 lanes, g.block / 64 waves, 2 targets per lane}, whose
+// rows have the same stride g.xr) first, then the matrix-core groups of `a`
+hipError_t launch_hybrid_sweep(int mode, const MfmaGeometry& g, int grid, const MfmaArgs& a,
+                               const SweepArgs& v, hipStream_t st);
+
 // log-likelihoods of the split blocks of a forward sweep
 hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,
                                     const double* svec, const int* sK, double* loglik,

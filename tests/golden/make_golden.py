@@ -155,7 +155,7 @@ INT_PARAMS = {
 INT_MODELS = {
     "ikat_1_1": ("ikat", 1, 1), "ikat_2_2": ("ikat", 2, 2), "ikat_3_3": ("ikat", 3, 3),
     "ialt_2_3": ("ialt", 2, 3), "ialt_3_2": ("ialt", 3, 2), "ikat_1_3": ("ikat", 1, 3),
-    "ikat_4_4": ("ikat", 4, 4),
+    "ikat_4_4": ("ikat", 4, 4), "ikat_5_5": ("ikat", 5, 5),
 }
 INT_ARGS = ("t_A", "t_B", "t_C", "t_2", "t_upper", "t_out", "t_m", "N_AB", "N_BC", "N_ABC",
             "r", "m")
