@@ -27,7 +27,7 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, diag: bool = False,
-          variant: str = "") -> str:
+          variant: str = "", extra_flags=None) -> str:
     """variant: an experiment build (libitrails_hip_<variant>.so, extra flags from
     ITR_HIPCC_FLAGS), loaded with ITR_LIB; never the product library."""
     out = OUT if not diag else OUT.replace(".so", "_diag.so")
@@ -37,7 +37,8 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False,
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-             "-fvisibility=hidden"] + os.environ.get("ITR_HIPCC_FLAGS", "").split()
+             "-fvisibility=hidden"] + (extra_flags if extra_flags is not None else
+                                       os.environ.get("ITR_HIPCC_FLAGS", "").split())
     if diag:
         flags += ["-DITR_DIAG"]
     tag = "_diag" if diag else (f"_{variant}" if variant else "")
@@ -61,4 +62,11 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False,
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))
+    if "--with-exp" in sys.argv:  # product + experiment library (env knobs), in parallel
+        import threading
+        t = threading.Thread(target=lambda: print(build(force=True, extra_flags=[])))
+        t.start()
+        print(build(variant="exp", extra_flags=["-DITR_EXPERIMENT"]))
+        t.join()
+    else:
+        print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))

@@ -130,11 +130,13 @@ struct itr_plan {
   // split blocks' scratch
   int64_t ntasks = 0, nsplit = 0;
   int32_t *d_tasks = nullptr, *d_split_blk = nullptr;
-  // hybrid (matrix-core) sweeps: the nurg longest blocks as VALU tasks (utasks: forward
-  // log-likelihood tasks; the posterior sweeps take order[0, nurg)), the rest as groups of
-  // four blocks in longest-first order
-  int64_t nurg = 0, nutasks = 0, ngroups = 0;
-  int32_t *d_utasks = nullptr, *d_groups = nullptr;
+  // hybrid (matrix-core) sweeps, see itr_plan_create: forward log-likelihood = VALU tasks
+  // utasks + matrix-core groups of task ids into mtasks (split slots hsplit_blk); posterior =
+  // VALU blocks order[0, nurg) + groups of four consecutive blocks of order[nurg, nblocks),
+  // nurg chosen per call from the state count (MfmaGeometry.pfrac)
+  int64_t nutasks = 0, ngroups_ll = 0, nhsplit = 0;
+  int32_t *d_utasks = nullptr, *d_mtasks = nullptr, *d_groups_ll = nullptr,
+          *d_hsplit_blk = nullptr;
   double* d_svec = nullptr;
   int* d_sK = nullptr;
   // workspace (grown on demand): forward rows (posterior) or the Viterbi checkpoint rows,
@@ -242,8 +244,21 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
                hipStream_t st, const char* tname) {
   itr::MfmaArgs a{};
   a.n = m->n;
-  a.ngroups = p->ngroups;
-  a.groups = p->d_groups;
+  const bool ll = mode == itr::MODE_FWD_LL;
+  int64_t nurg = 0;  // posterior: blocks longer than pfrac x the longest are VALU tasks
+  if (!ll) {
+    const double lim = std::max(512.0, g.pfrac * (double)(p->nblocks ? p->sorted_len[0] : 0));
+    while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
+    v.order = p->d_order;
+    v.nblocks = nurg;
+  }
+  a.ngroups = ll ? p->ngroups_ll : (p->nblocks - nurg + 3) / 4;
+  a.groups = ll ? p->d_groups_ll : p->d_order + nurg;
+  a.nmembers = ll ? 0 : p->nblocks - nurg;
+  a.tasks = p->d_mtasks;
+  a.matT = m->aT;
+  a.svec = p->d_svec;
+  a.sK = p->d_sK;
   a.queue = p->d_queue + 4;
   a.off = p->d_off;
   a.obs = v.obs;
@@ -257,7 +272,7 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   a.prio_len = INT32_MAX;
   v.queue = p->d_queue + 3;
   v.prio_len = 0;  // every VALU task of the hybrid is a long block: raised wave priority
-  const int64_t work = v.nblocks + (p->ngroups + g.gb - 1) / g.gb;
+  const int64_t work = v.nblocks + (a.ngroups + g.gb - 1) / g.gb;
   int per_cu = g.per_cu;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_HYB_PER_CU")) per_cu = atoi(getenv("ITR_HYB_PER_CU"));
@@ -269,7 +284,7 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   if (getenv("ITR_VERBOSE"))
     fprintf(stderr, "[itr] %s hybrid: n=%d cfg=%d block=%d per_cu=%d grid=%lld valu=%lld groups=%lld\n",
             tname, a.n, g.cfg, g.block, g.per_cu, (long long)grid, (long long)v.nblocks,
-            (long long)p->ngroups);
+            (long long)a.ngroups);
 #endif
   Scope sc(tname, st);
   HIP_TRY(itr::launch_hybrid_sweep(mode, g, (int)grid, a, v, st));
@@ -391,8 +406,7 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   // textbook backward over the second — whose vectors fwd_split_combine_kernel joins.
   // Tasks run longest first.  Two task lists over the same split blocks (slots):
   //   tasks   every block (the VALU-only sweep, state counts without a matrix-core form);
-  //   utasks  the `nurg` longest blocks only: the VALU part of the hybrid sweeps
-  //           (mfma_sweeps.hip), whose matrix-core groups take the remaining blocks.
+  //   the hybrid sweeps' own lists below.
   const int64_t tmax = nblocks ? h_off[order[0] + 1] - h_off[order[0]] : 0;
   std::vector<int32_t> split_blk;
   // ITR_SPLIT_FRAC (read once here, at plan creation): 0 disables the split (tests compare
@@ -435,35 +449,95 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
     return sorted;
   };
   std::vector<int32_t> tasks = make_tasks(nblocks);
-  // The hybrid sweeps' urgent set: blocks at least a quarter as long as the longest (and
-  // every split block).  A matrix-core group steps four blocks in about twice the VALU
-  // step time, so the longest blocks stay on the lower-latency VALU path while the bulk
-  // goes through the matrix cores.
-  double ufrac = 0.25;
+  // Hybrid sweeps (mfma_sweeps.hip).  A matrix-core group steps four blocks in about twice
+  // the VALU step time, so the longest work stays on the lower-latency VALU path and the
+  // bulk goes through the matrix cores.  Forward log-likelihood, with
+  // L = ufrac * longest:  T > 2L -> VALU tasks (split halves as above);  L < T <= 2L -> two
+  // matrix-core halves (first half forward, second half the textbook backward);  T <= L ->
+  // whole block in a matrix-core group.  (The posterior's split is chosen per call, run_hybrid.)
+  // Split slots of the hybrid forward are numbered separately (hsplit_blk).
+  // ufrac measured on the (5,5) model, 10 Mbp (scripts/gpu_r2b.sh: 0.12 / 0.18 / 0.22 / 0.25
+  // / 0.28 / 0.33 -> forward 4.93 / 4.24 / 3.97 / 3.85 / 3.80 / 3.97 ms)
+  double ufrac = 0.28;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_URGENT_FRAC")) ufrac = atof(getenv("ITR_URGENT_FRAC"));
 #endif
-  int64_t nurg = 0;
-  while (nurg < nblocks && (slot_of[order[nurg]] >= 0 ||
-                            (double)(h_off[order[nurg] + 1] - h_off[order[nurg]]) >=
-                                std::max(512.0, ufrac * (double)tmax)))
-    ++nurg;
-  p->nurg = nurg;
-  std::vector<int32_t> utasks = make_tasks(nurg);
-  std::vector<int32_t> groups;
-  for (int64_t k = nurg; k < nblocks; k += 4)
-    for (int64_t r = 0; r < 4; ++r) groups.push_back(k + r < nblocks ? order[k + r] : -1);
+  const double L = std::max(256.0, ufrac * (double)tmax);
+  std::vector<int32_t> hsplit_blk, utasks, mtasks;
+  std::vector<int64_t> ulen;
+  struct MT { int32_t id; int64_t steps; bool bwd; };
+  std::vector<MT> fwd_t, bwd_t;
+  for (int64_t k = 0; k < nblocks; ++k) {
+    const int32_t b = order[k];
+    const int64_t T = h_off[b + 1] - h_off[b];
+    if ((double)T > 2 * L) {
+      if (is_split(T)) {
+        const int32_t m = (int32_t)(T / 2), slot = (int32_t)hsplit_blk.size();
+        hsplit_blk.push_back(b);
+        utasks.insert(utasks.end(), {b, m, slot, b, -m, slot});
+        ulen.push_back(m);
+        ulen.push_back(T - m + 1);
+      } else {
+        utasks.insert(utasks.end(), {b, 0, 0});
+        ulen.push_back(T);
+      }
+    } else if ((double)T > L && T >= 512) {
+      const int32_t m = (int32_t)(T / 2), slot = (int32_t)hsplit_blk.size();
+      hsplit_blk.push_back(b);
+      fwd_t.push_back({(int32_t)(mtasks.size() / 3), m, false});
+      mtasks.insert(mtasks.end(), {b, m, slot});
+      bwd_t.push_back({(int32_t)(mtasks.size() / 3), T - m + 1, true});
+      mtasks.insert(mtasks.end(), {b, -m, slot});
+    } else {
+      fwd_t.push_back({(int32_t)(mtasks.size() / 3), T, false});
+      mtasks.insert(mtasks.end(), {b, 0, 0});
+    }
+  }
+  {  // VALU tasks longest first
+    std::vector<int64_t> idx(ulen.size());
+    std::iota(idx.begin(), idx.end(), 0);
+    std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return ulen[x] > ulen[y]; });
+    std::vector<int32_t> sorted(utasks.size());
+    for (size_t k = 0; k < idx.size(); ++k)
+      for (int c = 0; c < 3; ++c) sorted[3 * k + c] = utasks[3 * idx[k] + c];
+    utasks.swap(sorted);
+  }
+  // matrix-core groups: forward-shaped tasks and second halves grouped separately (a group
+  // shares its matrix operand), longest first, merged two groups at a time so that a
+  // workgroup running two groups (GB = 2) always gets two of one kind
+  auto by_steps = [](const MT& x, const MT& y) { return x.steps > y.steps; };
+  std::stable_sort(fwd_t.begin(), fwd_t.end(), by_steps);
+  std::stable_sort(bwd_t.begin(), bwd_t.end(), by_steps);
+  std::vector<int32_t> groups_ll;
+  {
+    size_t fi = 0, bi2 = 0;
+    auto take_group = [&](std::vector<MT>& v, size_t& i) {
+      for (int r = 0; r < 4; ++r) groups_ll.push_back(i < v.size() ? v[i++].id : -1);
+    };
+    while (fi < fwd_t.size() || bi2 < bwd_t.size()) {
+      const bool pick_f = bi2 >= bwd_t.size() ||
+                          (fi < fwd_t.size() && fwd_t[fi].steps >= bwd_t[bi2].steps);
+      for (int g = 0; g < 2; ++g) {
+        if (pick_f) take_group(fwd_t, fi);
+        else take_group(bwd_t, bi2);
+      }
+    }
+  }
+  p->nutasks = (int64_t)utasks.size() / 3;
+  p->ngroups_ll = (int64_t)groups_ll.size() / 4;
+  p->nhsplit = (int64_t)hsplit_blk.size();
   p->ntasks = (int64_t)tasks.size() / 3;
   p->nsplit = (int64_t)split_blk.size();
-  p->nutasks = (int64_t)utasks.size() / 3;
-  p->ngroups = (int64_t)groups.size() / 4;
   int e = 0;
   if (!e) e = dev_alloc(&p->d_tasks, tasks.size());
   if (!e) e = dev_alloc(&p->d_utasks, utasks.size());
-  if (!e) e = dev_alloc(&p->d_groups, groups.size());
+  if (!e) e = dev_alloc(&p->d_mtasks, mtasks.size());
+  if (!e) e = dev_alloc(&p->d_groups_ll, groups_ll.size());
+  if (!e) e = dev_alloc(&p->d_hsplit_blk, hsplit_blk.size());
   if (!e) e = dev_alloc(&p->d_split_blk, split_blk.size());
-  if (!e) e = dev_alloc(&p->d_svec, (size_t)p->nsplit * 2 * 256);
-  if (!e) e = dev_alloc(&p->d_sK, (size_t)p->nsplit * 2);
+  const size_t nslots = (size_t)std::max(p->nsplit, p->nhsplit);
+  if (!e) e = dev_alloc(&p->d_svec, nslots * 2 * 256);
+  if (!e) e = dev_alloc(&p->d_sK, nslots * 2);
   if (!e) e = dev_alloc(&p->d_off, nblocks + 1);
   if (!e) e = dev_alloc(&p->d_tile_off, nblocks + 1);
   if (!e) e = dev_alloc(&p->d_order, nblocks);
@@ -480,7 +554,9 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   up(p->d_order, order.data(), nblocks * sizeof(int32_t));
   up(p->d_tasks, tasks.data(), tasks.size() * sizeof(int32_t));
   up(p->d_utasks, utasks.data(), utasks.size() * sizeof(int32_t));
-  up(p->d_groups, groups.data(), groups.size() * sizeof(int32_t));
+  up(p->d_mtasks, mtasks.data(), mtasks.size() * sizeof(int32_t));
+  up(p->d_groups_ll, groups_ll.data(), groups_ll.size() * sizeof(int32_t));
+  up(p->d_hsplit_blk, hsplit_blk.data(), hsplit_blk.size() * sizeof(int32_t));
   up(p->d_split_blk, split_blk.data(), split_blk.size() * sizeof(int32_t));
   if (e) {
     itr_plan_destroy(p);
@@ -500,7 +576,9 @@ int itr_plan_destroy(itr_plan_t p) {
   dev_free(p->d_stay);
   dev_free(p->d_tasks);
   dev_free(p->d_utasks);
-  dev_free(p->d_groups);
+  dev_free(p->d_mtasks);
+  dev_free(p->d_groups_ll);
+  dev_free(p->d_hsplit_blk);
   dev_free(p->d_split_blk);
   dev_free(p->d_svec);
   dev_free(p->d_sK);
@@ -543,14 +621,15 @@ int itr_forward_loglik(itr_model_t m, itr_plan_t p, const uint16_t* obs, double*
     return fail(ITR_ESTATE, "forward task tables missing");
   const itr::MfmaGeometry g = itr::mfma_geometry(m->n, itr::MODE_FWD_LL);
   int xr = itr::sweep_row_stride(m->n, itr::MODE_FWD_LL);
-  if (g.cfg >= 0 && p->ngroups > 0) {
+  if (g.cfg >= 0 && p->ngroups_ll > 0) {
     a.tasks = p->d_utasks;
     a.nblocks = p->nutasks;
-    xr = g.xr;
     if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, st, "forward")) return e;
-  } else {
-    if (int e = run_sweep(itr::MODE_FWD_LL, a, st, "forward")) return e;
+    HIP_TRY(itr::launch_fwd_split_combine(m->n, g.xr, (int)p->nhsplit, p->d_hsplit_blk,
+                                          p->d_svec, p->d_sK, loglik, st));
+    return 0;
   }
+  if (int e = run_sweep(itr::MODE_FWD_LL, a, st, "forward")) return e;
   HIP_TRY(itr::launch_fwd_split_combine(m->n, xr, (int)p->nsplit, p->d_split_blk, p->d_svec,
                                         p->d_sK, loglik, st));
   return 0;
@@ -610,10 +689,9 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
   a.init = m->PIE;
   a.alpha = p->d_alpha;
   const itr::MfmaGeometry g = itr::mfma_geometry(m->n, itr::MODE_FWD_STORE);
-  if (g.cfg >= 0 && p->ngroups > 0) {
+  if (g.cfg >= 0) {
     // forward rows at the hybrid's stride g.xr for every block (reserve() sized for it)
     const itr::MfmaGeometry gb = itr::mfma_geometry(m->n, itr::MODE_BWD);
-    a.nblocks = p->nurg;  // the VALU part: order[0, nurg)
     if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, st, "posterior_fwd")) return e;
     a.post = post;
     return run_hybrid(itr::MODE_BWD, m, p, a, gb, st, "posterior_bwd");

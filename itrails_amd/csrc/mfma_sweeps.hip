@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -66,6 +67,14 @@ struct MOcc {
   static constexpr int value = wgs * ((NT + 3) / 4);  // waves per SIMD (busiest SIMD)
 };
 
+// member rr of group gi (-1: none); with p.nmembers > 0 the groups are consecutive
+// 4-chunks of a list of p.nmembers entries (the posterior's longest-first block order)
+__device__ __forceinline__ int group_member(const MfmaArgs& p, int gi, int rr) {
+  const int64_t k = 4 * (int64_t)gi + rr;
+  if (gi >= p.ngroups || (p.nmembers > 0 && k >= p.nmembers)) return -1;
+  return p.groups[k];
+}
+
 // LDS of one matrix-core task (carved from the kernel's dynamic LDS)
 template <int NT, int NK, int GB>
 struct MLds {
@@ -100,47 +109,76 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
   const bool jv = j < n;
   const bool row_leader = (l & 15) == 0;
 
-  double B[NK];  // this lane's slice of a: rows kk*NK + s, column j (per task: a few L2
-                 // loads against thousands of steps, and nothing live across tasks)
+  // Rows of the group(s).  MODE_FWD_LL: p.groups holds task ids of p.tasks {block, split,
+  // slot} — whole blocks (split 0), first halves (split m > 0: columns [0, m)) or second
+  // halves (split -m: the textbook backward from the end, contracting with a^T, see
+  // valu_sweep.h); a group is all forward-shaped or all backward halves.  Other modes:
+  // block ids.  T = steps of the row, Tb = block length, dir = column order.
+  int T[GB], Tb[GB], dir[GB], Tmax = 0;
+  int64_t c0[GB];
+  int task_blk[GB], task_split[GB], task_slot[GB];
+  bool backward_group = false;
+#pragma unroll
+  for (int gb = 0; gb < GB; ++gb) {
+    const int gi = g0 + gb;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int id = group_member(p, gi, rr);
+      int b2 = id, sp = 0, sl = 0;
+      if (MODE == MODE_FWD_LL && id >= 0) {
+        b2 = p.tasks[3 * id];
+        sp = p.tasks[3 * id + 1];
+        sl = p.tasks[3 * id + 2];
+      }
+      const int tb2 = b2 >= 0 ? (int)(p.off[b2 + 1] - p.off[b2]) : 0;
+      const int t2 = sp > 0 ? sp : (sp < 0 ? tb2 + sp + 1 : tb2);
+      Tmax = max(Tmax, t2);
+      if (rr == 0 && sp < 0) backward_group = true;
+      if (rr == r) {
+        task_blk[gb] = b2;
+        task_split[gb] = sp;
+        task_slot[gb] = sl;
+        Tb[gb] = tb2;
+        T[gb] = t2;
+        dir[gb] = sp < 0 ? -1 : 1;
+        c0[gb] = b2 >= 0 ? p.off[b2] : 0;
+      }
+    }
+  }
+  Tmax = uni(Tmax);
+  backward_group = uni(backward_group);
+  (void)task_slot;
+  (void)task_blk;
+
+  double B[NK];  // this lane's slice of a (a^T for backward halves): rows kk*NK + s,
+                 // column j (per task: a few L2 loads against thousands of steps)
+  const double* mp = (MODE == MODE_FWD_LL && backward_group) ? p.matT : p.mat;
 #pragma unroll
   for (int s = 0; s < NK; ++s) {
     const int i = kk * NK + s;
-    B[s] = (i < n && jv) ? p.mat[(int64_t)i * n + j] : 0.0;
+    B[s] = (i < n && jv) ? mp[(int64_t)i * n + j] : 0.0;
   }
   for (int i = tid; i < GB * 2 * 4 * KP; i += TB) (&X[0][0][0][0])[i] = 0.0;
   lds_barrier();
   {
-    // this lane's block in each of its groups, and the lock-step length
-    int T[GB], Tmax = 0;
-    int64_t c0[GB];
-    int blk[GB];
-#pragma unroll
-    for (int gb = 0; gb < GB; ++gb) {
-      const int gi = g0 + gb;
-      blk[gb] = gi < p.ngroups ? p.groups[4 * gi + r] : -1;
-      c0[gb] = blk[gb] >= 0 ? p.off[blk[gb]] : 0;
-      T[gb] = blk[gb] >= 0 ? (int)(p.off[blk[gb] + 1] - c0[gb]) : 0;
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int b2 = gi < p.ngroups ? p.groups[4 * gi + rr] : -1;
-        const int T2 = b2 >= 0 ? (int)(p.off[b2 + 1] - p.off[b2]) : 0;
-        Tmax = max(Tmax, T2);
-      }
-    }
-    Tmax = uni(Tmax);
     if (MODE == MODE_FWD_LL && Tmax == 0 && tid < 4 * GB) {  // only empty blocks: log 1 = 0
       const int gi = g0 + (tid >> 2);
-      const int b2 = gi < p.ngroups ? p.groups[4 * gi + (tid & 3)] : -1;
-      if (b2 >= 0) p.loglik[b2] = 0.0;
+      const int id = group_member(p, gi, tid & 3);
+      if (id >= 0) p.loglik[p.tasks[3 * id]] = 0.0;
     }
     if (Tmax > 0) {
       const bool urgent = Tmax >= p.prio_len;
       if (urgent) __builtin_amdgcn_s_setprio(2);
-      // symbol of column t of this lane's block, clamped into the block (forward: t; the
-      // backward sweep asks for T - 1 - s)
-      auto sym = [&](int gb, int t) -> int {
-        const int tc = min(max(t, 0), max(T[gb] - 1, 0));
-        return T[gb] > 0 ? min((int)p.obs[c0[gb] + tc], 624) : 0;
+      // symbol of step s of this lane's row: column s (forward) or Tb - 1 - s (backward),
+      // clamped into the block; -2 = a row of ones (a backward half's last step)
+      auto sym = [&](int gb, int s) -> int {
+        if (MODE == MODE_FWD_LL && task_split[gb] < 0 && s == T[gb] - 1) return -2;
+        const int t = dir[gb] > 0 ? s : Tb[gb] - 1 - s;
+        const int tc = min(max(t, 0), max(Tb[gb] - 1, 0));
+        return Tb[gb] > 0 ? min((int)p.obs[c0[gb] + tc], 624) : 0;
+      };
+      auto emis = [&](int sy) -> double {
+        return jv ? (sy < 0 ? 1.0 : p.emit[sy * n + j]) : 0.0;
       };
       int snxt[GB][TE];
       double enxt[GB][TE];
@@ -151,14 +189,16 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
         int K[GB], Kfin[GB];
 #pragma unroll
         for (int gb = 0; gb < GB; ++gb) {
-          x[gb] = (T[gb] > 0 && jv) ? p.init[sym(gb, 0) * n + j] : 0.0;
+          // x_0 = pi * e_0 (forward rows); a backward half starts from e_{Tb-1}
+          const double* x0tab = dir[gb] < 0 ? p.emit : p.init;
+          x[gb] = (T[gb] > 0 && jv) ? x0tab[sym(gb, 0) * n + j] : 0.0;
           if (jv) X[gb][0][r][j] = x[gb];
           if (MODE == MODE_FWD_STORE && T[gb] > 0) p.alpha[c0[gb] * p.astride + j] = x[gb];
           xfin[gb] = x[gb];
           K[gb] = Kfin[gb] = 0;
 #pragma unroll
           for (int u = 0; u < TE; ++u) {
-            enxt[gb][u] = jv ? p.emit[sym(gb, u) * n + j] : 0.0;
+            enxt[gb][u] = emis(sym(gb, u));
             snxt[gb][u] = sym(gb, TE + u);
           }
         }
@@ -172,7 +212,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
             for (int u = 0; u < TE; ++u) ecur[gb][u] = enxt[gb][u];
 #pragma unroll
             for (int u = 0; u < TE; ++u) {
-              enxt[gb][u] = jv ? p.emit[snxt[gb][u] * n + j] : 0.0;
+              enxt[gb][u] = emis(snxt[gb][u]);
               snxt[gb][u] = sym(gb, t0 + 2 * TE + u);
             }
           }
@@ -228,9 +268,16 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
           }
         }
         if constexpr (MODE == MODE_FWD_LL) {
-          // log P = log(sum_j x_j) + K ln 2   (optimizer.py:160-162)
 #pragma unroll
           for (int gb = 0; gb < GB; ++gb) {
+            if (task_split[gb] != 0) {
+              // half of a split block: the scaled vector and its exponent
+              // (fwd_split_combine_kernel joins the halves)
+              const int side = task_split[gb] < 0;
+              if (jv) p.svec[((int64_t)task_slot[gb] * 2 + side) * p.astride + j] = xfin[gb];
+              if (w == 0 && row_leader) p.sK[task_slot[gb] * 2 + side] = Kfin[gb];
+            }
+            // log P = log(sum_j x_j) + K ln 2   (optimizer.py:160-162)
             const double s = row16_sum(xfin[gb]);
             if (row_leader) RS[gb][0][w][r] = s;
             if (w == 0 && row_leader) KF[gb][r] = Kfin[gb];
@@ -239,8 +286,9 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
           if (tid < 4 * GB) {
             const int gb = tid >> 2, rr = tid & 3;
             const int gi = g0 + gb;
-            const int b2 = gi < p.ngroups ? p.groups[4 * gi + rr] : -1;
-            if (b2 >= 0) {
+            const int id = group_member(p, gi, rr);
+            if (id >= 0 && p.tasks[3 * id + 1] == 0) {
+              const int b2 = p.tasks[3 * id];
               double S = 0.0;
               for (int v = 0; v < NT; ++v) S += RS[gb][0][v][rr];
               const int T2 = (int)(p.off[b2 + 1] - p.off[b2]);
@@ -310,7 +358,8 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
                 double S = RS[gb][buf][0][r];
 #pragma unroll
                 for (int v = 1; v < NT; ++v) S += RS[gb][buf][v][r];
-                if (s < T[gb] && jv) p.post[(c0[gb] + (T[gb] - 1 - s)) * n + j] = qv[gb] / S;
+                const double rS = 1.0 / S;
+                if (s < T[gb] && jv) p.post[(c0[gb] + (T[gb] - 1 - s)) * n + j] = qv[gb] * rS;
                 double sc = 1.0;
                 if (sub == 0 && (s0 & 7) == 0) {
                   double M = RM[gb][0][r];
@@ -371,10 +420,21 @@ __global__ void __launch_bounds__(64 * NT, (MOcc<NT, NK, GB, MODE>::value))
 // ---------------------------------------------------------------------------------------
 struct MCfg {
   int nmin, nmax, nt, nk, gb, viq;  // viq: sources per lane of the VALU tasks (8 lanes)
+  double pfrac;  // posterior: blocks longer than pfrac x the longest run as VALU tasks
+  bool post;     // the hybrid posterior beats the VALU-only one at this size
 };
+// pfrac measured on the (7,7) model, 10 Mbp (scripts/gpu_post133.sh: 0.2 / 0.35 / 0.5 / 0.7
+// -> 203 / 264 / 281 / 259 M columns/s) and the (5,5) model (scripts/gpu_r2b.sh)
+// (the (5,5) model, N = 70: hybrid posterior 465 M columns/s against 496 for the VALU-only
+// three-wave sweeps, so the posterior stays VALU-only up to N = 96)
 constexpr MCfg kMCfgs[] = {
-    {33, 48, 3, 12, 1, 6}, {49, 64, 4, 16, 1, 8}, {65, 72, 5, 18, 1, 9}, {73, 80, 5, 20, 1, 10},
-    {81, 96, 6, 24, 1, 12}, {129, 136, 9, 34, 2, 17}, {137, 144, 9, 36, 2, 18}};
+    {33, 48, 3, 12, 1, 6, 0.35, false},   {49, 64, 4, 16, 1, 8, 0.35, false},
+    {65, 72, 5, 18, 1, 9, 0.35, false},   {73, 80, 5, 20, 1, 10, 0.35, false},
+    {81, 96, 6, 24, 1, 12, 0.35, false},  {129, 136, 9, 34, 1, 17, 0.5, true},
+    {137, 144, 9, 36, 1, 18, 0.5, true},
+    // two groups per workgroup (experiment configuration, ITR_MCFG)
+    {129, 136, 9, 34, 2, 17, 0.5, true}};
+constexpr int kMCfgsAuto = 7;  // entries picked by state count
 
 template <int NT, int NK, int GB, int MODE, int VIQ>
 size_t lds_h() {
@@ -412,8 +472,9 @@ hipError_t dispatch_m(int c, bool launch, const MfmaArgs* a, const SweepArgs* v,
     ITR_MCFG(2, 5, 18, 1, 9)
     ITR_MCFG(3, 5, 20, 1, 10)
     ITR_MCFG(4, 6, 24, 1, 12)
-    ITR_MCFG(5, 9, 34, 2, 17)
-    ITR_MCFG(6, 9, 36, 2, 18)
+    ITR_MCFG(5, 9, 34, 1, 17)
+    ITR_MCFG(6, 9, 36, 1, 18)
+    ITR_MCFG(7, 9, 34, 2, 17)
   }
 #undef ITR_MCFG
   return hipErrorInvalidValue;
@@ -435,12 +496,30 @@ MfmaGeometry mfma_geometry(int n, int mode) {
   MfmaGeometry g{};
   g.cfg = -1;
   if (mode == MODE_VIT) return g;  // max-plus: no matrix-core form
-  for (int c = 0; c < (int)(sizeof kMCfgs / sizeof kMCfgs[0]); ++c)
+  for (int c = 0; c < kMCfgsAuto; ++c)
     if (n >= kMCfgs[c].nmin && n <= kMCfgs[c].nmax) g.cfg = c;
+  if (g.cfg >= 0 && mode != MODE_FWD_LL && !kMCfgs[g.cfg].post) g.cfg = -1;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_NO_MFMA")) g.cfg = -1;
+  if (getenv("ITR_HYB_POST") && mode != MODE_FWD_LL) {  // force the hybrid posterior
+    for (int c = 0; c < kMCfgsAuto; ++c)
+      if (n >= kMCfgs[c].nmin && n <= kMCfgs[c].nmax) g.cfg = c;
+  }
+  if (getenv("ITR_MCFG")) {
+    const int c = atoi(getenv("ITR_MCFG"));
+    if (c >= 0 && c < (int)(sizeof kMCfgs / sizeof kMCfgs[0]) && n >= kMCfgs[c].nmin &&
+        n <= kMCfgs[c].nmax)
+      g.cfg = c;
+  }
+#endif
   if (g.cfg < 0) return g;
   g.block = 64 * kMCfgs[g.cfg].nt;
   g.xr = 16 * kMCfgs[g.cfg].nt;
   g.gb = kMCfgs[g.cfg].gb;
+  g.pfrac = kMCfgs[g.cfg].pfrac;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_POST_URGENT_FRAC")) g.pfrac = atof(getenv("ITR_POST_URGENT_FRAC"));
+#endif
   int occ = 1;
   (void)dispatch_mode_m(mode, g.cfg, false, nullptr, nullptr, 0, nullptr, &occ);
   g.per_cu = occ;

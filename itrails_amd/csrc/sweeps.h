@@ -61,17 +61,23 @@ hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepA
 struct MfmaArgs {
   int n;                        // hidden states
   int64_t ngroups;
-  const int32_t* groups;        // [ngroups x 4] block ids, longest group first (-1: none)
+  const int32_t* groups;        // [ngroups x 4] longest group first (-1: none): task ids of
+                                //   `tasks` (MODE_FWD_LL) or block ids (other modes)
+  int64_t nmembers;             // > 0: groups = consecutive 4-chunks of this many entries
+  const int32_t* tasks;         // MODE_FWD_LL: {block, split, slot} (see SweepArgs.tasks)
   int* queue;                   // work counter, zero at launch
   const int64_t* off;           // [nblocks+1]
   const uint16_t* obs;          // [total]
   const double* mat;            // a, n x n
+  const double* matT;           // a^T (MODE_FWD_LL: groups of second halves)
   const double* emit;           // E, 625 x n
   const double* init;           // pi*E, 625 x n
   double* loglik;               // [nblocks]                  (MODE_FWD_LL)
   double* alpha;                // forward rows, row stride astride (FWD_STORE out, BWD in)
   int64_t astride;
   double* post;                 // [total x n]                (MODE_BWD)
+  double* svec;                 // MODE_FWD_LL: split halves' vectors [slots x 2 x astride]
+  int* sK;                      // MODE_FWD_LL: their power-of-two exponents [slots x 2]
   int prio_len;                 // groups at least this long run at raised wave priority
 };
 struct MfmaGeometry {
@@ -80,6 +86,7 @@ struct MfmaGeometry {
   int xr;       // padded targets (row stride of stored forward rows >= xr)
   int gb;       // groups per workgroup
   int per_cu;   // resident workgroups per CU (occupancy API)
+  double pfrac; // posterior sweeps: blocks longer than pfrac x the longest are VALU tasks
 };
 MfmaGeometry mfma_geometry(int n, int mode);
 // one launch: the VALU tasks of `v` (v.tasks / v.order, v.nblocks of them: the longest

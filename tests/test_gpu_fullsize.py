@@ -120,3 +120,54 @@ def test_full_size_posterior_host_copy(full):
     assert np.array_equal(np.concatenate(host), post)
     del post, host
     torch.cuda.empty_cache()
+
+
+# ---------------------------------------------------------------------------------------
+# BASELINE config 3: the reference's own (7,7) model (N = 133, tests/golden/model_kat_7_7.npz,
+# 3,638 s of reference build), 10 Mbp, posterior decoding (+ forward and Viterbi)
+# ---------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def full77(gpu):
+    import torch
+    g = golden("model_kat_7_7.npz")
+    a, b, pi = g["a"], g["b"], g["pi"]
+    rng = np.random.default_rng(12345)  # bench.py's layout
+    lengths = block_lengths(rng, 10_000_000, 2000.0)
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=777)
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).cuda()
+    lens = np.diff(off)
+    longest = np.argsort(-lens, kind="stable")[:6]
+    sample = np.unique(np.concatenate([longest, np.random.default_rng(6).choice(len(lens), 24,
+                                                                                replace=False)]))
+    return dict(a=a, b=b, pi=pi, obs=obs, off=off, model=model, plan=plan, d_obs=d_obs,
+                sample=sample, t=build_tables(a, b, pi))
+
+
+def test_full_size_77_posterior(full77):
+    """Every posterior row of the 10 Mbp alignment sums to 1 (1e-12); the longest blocks and
+    a seeded sample match the CPU restatement to 1e-8."""
+    import torch
+    f = full77
+    f["plan"].reserve(133, posterior=True)
+    post = hmm.posterior_device(f["model"], f["plan"], f["d_obs"])
+    assert float((post.sum(dim=1) - 1.0).abs().max()) < 1e-12
+    so, soff = _sub(f["obs"], f["off"], f["sample"])
+    ref = O.posterior(f["t"], so, soff)
+    off = f["off"]
+    rows = torch.cat([post[off[k]:off[k + 1]] for k in f["sample"]]).cpu().numpy()
+    np.testing.assert_allclose(rows, ref, rtol=1e-8, atol=1e-300)
+    del post
+    torch.cuda.empty_cache()
+
+
+def test_full_size_77_forward_viterbi(full77):
+    f = full77
+    ll = hmm.forward_loglik_device(f["model"], f["plan"], f["d_obs"]).cpu().numpy()
+    path = hmm.viterbi_device(f["model"], f["plan"], f["d_obs"]).cpu().numpy()
+    assert np.isfinite(ll).all() and (ll < 0).all()
+    so, soff = _sub(f["obs"], f["off"], f["sample"])
+    np.testing.assert_allclose(ll[f["sample"]], O.forward_loglik(f["t"], so, soff), rtol=1e-8,
+                               atol=0)
+    got = np.concatenate([path[f["off"][k]:f["off"][k + 1]] for k in f["sample"]])
+    np.testing.assert_array_equal(got, O.viterbi(f["t"], so, soff))
