@@ -169,8 +169,13 @@ int check_plan(itr_plan_t p) {
 
 // Workspace: Viterbi = one checkpoint row (f64) and one flag word (u16) per state per
 // 16-column tile record; posterior = the forward rows of every column.
+int vit_stride(int n) {  // record stride of the Viterbi workspace for this state count
+  const itr::VitHybridGeometry vh = itr::vit_hybrid_geometry(n);
+  return vh.cfg >= 0 ? vh.xr : itr::sweep_row_stride(n, itr::MODE_VIT);
+}
+
 int reserve(itr_plan_t p, int n, bool vit, bool post) {
-  const int xr = itr::sweep_row_stride(n, itr::MODE_VIT);
+  const int xr = vit_stride(n);
   const int xa = itr::sweep_row_stride(n, itr::MODE_BWD);
   if (xr < 0 || xa < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", n);
   size_t need_rows = 0;
@@ -651,10 +656,30 @@ int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
   a.alpha = p->d_alpha;
   a.stay = p->d_stay;
   a.last_state = p->d_last;
-  if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
+  const itr::VitHybridGeometry vh = itr::vit_hybrid_geometry(m->n);
+  if (vh.cfg >= 0) {
+    // the longest blocks (longer than vfrac x the longest) as VALU tasks, the rest in
+    // lock-step groups; one workgroup per CU
+    double vfrac = 0.35;
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_VIT_URGENT_FRAC")) vfrac = atof(getenv("ITR_VIT_URGENT_FRAC"));
+#endif
+    const double lim = std::max(512.0, vfrac * (double)p->sorted_len[0]);
+    int64_t nurg = 0;
+    while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
+    a.queue = p->d_queue + 5;
+    a.prio_len = 0;
+    const int64_t work = nurg + (p->nblocks - nurg + vh.G - 1) / vh.G;
+    const int64_t grid = std::min<int64_t>(cu_count(), work);
+    HIP_TRY(hipMemsetAsync(p->d_queue + 5, 0, 2 * sizeof(int), st));
+    Scope sc("viterbi", st);
+    HIP_TRY(itr::launch_vit_hybrid(vh, (int)grid, a, (int)nurg, st));
+  } else {
+    if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
+  }
   itr::TraceArgs ta{};
   ta.n = m->n;
-  ta.xr = itr::sweep_row_stride(m->n, itr::MODE_VIT);
+  ta.xr = vit_stride(m->n);
   ta.nblocks = p->nblocks;
   ta.off = p->d_off;
   ta.tile_off = p->d_tile_off;

@@ -95,6 +95,20 @@ MfmaGeometry mfma_geometry(int n, int mode);
 hipError_t launch_hybrid_sweep(int mode, const MfmaGeometry& g, int grid, const MfmaArgs& a,
                                const SweepArgs& v, hipStream_t st);
 
+// Viterbi hybrid (vit_hybrid.hip): the longest blocks as VALU tasks, the bulk as groups of
+// G blocks in lock-step, two lanes per (block, target)
+struct VitHybridGeometry {
+  int cfg;      // configuration (negative: none for this n)
+  int block;    // threads per workgroup
+  int xr;       // record stride of the checkpoint rows / flag words
+  int G;        // blocks per lock-step group
+  size_t lds;   // dynamic LDS bytes
+};
+VitHybridGeometry vit_hybrid_geometry(int n);
+// v.order[0, nurg) as VALU tasks, then groups of v.order[nurg, v.nblocks); v.queue[0..1]
+hipError_t launch_vit_hybrid(const VitHybridGeometry& g, int grid, const SweepArgs& v, int nurg,
+                             hipStream_t st);
+
 // log-likelihoods of the split blocks of a forward sweep
 hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,
                                     const double* svec, const int* sK, double* loglik,

@@ -650,6 +650,9 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
 #pragma unroll
                 for (int r = 0; r < RJN; ++r) ec[r] = staged(EST, t, jr[r]);
               }
+              // waves whose targets are all padding (the Viterbi hybrid runs this task on a
+              // wider workgroup than the block needs) skip the arithmetic: a uniform branch
+              if (w * JW < n) {
               const double* xs = Xb + q * IQS;
               // NCH independent max chains per target (k = c mod NCH)
               double bc[NCH][RJN];
@@ -682,6 +685,7 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
                 bits[r] |= (uint32_t)(yd > yo) << sub;
                 x[r] = fmax(yd, yo);
               }
+              }  // w * JW < n
               STAMP(4);
               if (sub == 0 && q == 0) {  // the tile's checkpoint row (t = t0 >= 16)
 #pragma unroll
