@@ -161,8 +161,7 @@ def pmc_traffic(n, mode, tag_hint=""):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
     of this command (scripts/gpu_round.sh -> scripts/summarize_profile.py ->
     profiles/*_summary.json: FETCH_SIZE + WRITE_SIZE from separate passes, raw)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")),
-                   key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))  # by round tag
     for f in reversed(files):
         d = json.load(open(f))
         for name, v in d.items():
