@@ -86,6 +86,11 @@ def lib():
         raise ImportError(
             f"{LIB_PATH} is missing: build the HIP extension first "
             "(python -c 'import __graft_entry__ as g; g.build()')")
+    # One HIP runtime per process: torch (device memory, streams) is loaded first, so the
+    # library's libamdhip64.so.7 resolves to the runtime torch already mapped.  Loaded the
+    # other way round, /opt/rocm's runtime and torch's bundled one both open the device and
+    # the second reports "no ROCm-capable device".
+    import torch  # noqa: F401
     L = ctypes.CDLL(LIB_PATH)
     for name, (args, res) in _SIGNATURES.items():
         f = getattr(L, name)

@@ -121,6 +121,7 @@ struct itr_plan {
   int64_t ntiles = 0;            // Viterbi tile records: sum over blocks of ceil(T / 16)
   int64_t* d_off = nullptr;
   int64_t* d_tile_off = nullptr;  // [nblocks+1] first tile record of every block
+  int* d_cubusy = nullptr;        // [4096] per-CU long-block counts (Viterbi hybrid)
   int32_t* d_order = nullptr;
   int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
@@ -545,6 +546,9 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   if (!e) e = dev_alloc(&p->d_sK, nslots * 2);
   if (!e) e = dev_alloc(&p->d_off, nblocks + 1);
   if (!e) e = dev_alloc(&p->d_tile_off, nblocks + 1);
+  if (!e) e = dev_alloc(&p->d_cubusy, 4096);
+  if (!e && hipMemset(p->d_cubusy, 0, 4096 * sizeof(int)) != hipSuccess)
+    e = fail(ITR_EHIP, "plan workspace init failed");
   if (!e) e = dev_alloc(&p->d_order, nblocks);
   if (!e) e = dev_alloc(&p->d_queue, 8);
   if (!e) e = dev_alloc(&p->d_sink, 64);
@@ -575,6 +579,7 @@ int itr_plan_destroy(itr_plan_t p) {
   if (!p) return 0;
   dev_free(p->d_off);
   dev_free(p->d_tile_off);
+  dev_free(p->d_cubusy);
   dev_free(p->d_order);
   dev_free(p->d_queue);
   dev_free(p->d_sink);
@@ -670,10 +675,10 @@ int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
     a.queue = p->d_queue + 5;
     a.prio_len = 0;
     const int64_t work = nurg + (p->nblocks - nurg + vh.G - 1) / vh.G;
-    const int64_t grid = std::min<int64_t>(cu_count(), work);
+    const int64_t grid = std::min<int64_t>((int64_t)vh.per_cu * cu_count(), work);
     HIP_TRY(hipMemsetAsync(p->d_queue + 5, 0, 2 * sizeof(int), st));
     Scope sc("viterbi", st);
-    HIP_TRY(itr::launch_vit_hybrid(vh, (int)grid, a, (int)nurg, st));
+    HIP_TRY(itr::launch_vit_hybrid(vh, (int)grid, a, (int)nurg, p->d_cubusy, st));
   } else {
     if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
   }

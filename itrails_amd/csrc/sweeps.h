@@ -103,11 +103,14 @@ struct VitHybridGeometry {
   int xr;       // record stride of the checkpoint rows / flag words
   int G;        // blocks per lock-step group
   size_t lds;   // dynamic LDS bytes
+  int per_cu;   // resident workgroups per CU
+  int exit_busy;  // bulk workgroups on a CU decoding a long block: 0 wait, 1 exit, -1 ignore
 };
 VitHybridGeometry vit_hybrid_geometry(int n);
 // v.order[0, nurg) as VALU tasks, then groups of v.order[nurg, v.nblocks); v.queue[0..1]
+// cu_busy: [4096] per-CU counts of long blocks in progress (zero between launches)
 hipError_t launch_vit_hybrid(const VitHybridGeometry& g, int grid, const SweepArgs& v, int nurg,
-                             hipStream_t st);
+                             int* cu_busy, hipStream_t st);
 
 // log-likelihoods of the split blocks of a forward sweep
 hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,

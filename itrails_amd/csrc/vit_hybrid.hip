@@ -36,33 +36,45 @@ namespace itr {
 #ifdef ITR_EXPERIMENT
 namespace {
 
-// LDS of a bulk group task: X[2][G][2*IQ2] published omega vectors, Y[G][2*IQ2] last rows
-template <int W, int IQ2>
+// LDS of a bulk group task: X[2][GM][XB] published omega vectors, Y[GM][XB] last rows
+template <int W, int QL, int IQ>
 struct VLds {
-  static constexpr int XB = 2 * IQ2;
-  static constexpr int G = (64 * W) / (2 * (2 * IQ2 - 1));  // blocks per group (upper bound)
-  static constexpr size_t bytes = (size_t)(2 * G + G) * XB * 8;
+  static constexpr int XB = QL * IQ + (QL * IQ) % 2;
+  static constexpr int GM = (64 * W) / (QL * (QL * (IQ - 1) + 1));  // blocks per group (max)
+  static constexpr size_t bytes = (size_t)3 * GM * XB * 8;
 };
 
-// One bulk task: blocks grp[0 .. G) (-1: none) of at most 2*IQ2 states, G = (64W) / (2n).
-template <int W, int IQ2>
+// Key of the CU this wave runs on (XCC, shader engine, shader array, CU): the bulk
+// workgroups leave a CU on which a long block is being decoded (cu_busy[key] > 0), so the
+// long block steps alone.  Placement information for speed only, never for correctness.
+__device__ __forceinline__ int cu_key() {
+  const unsigned hw = __builtin_amdgcn_s_getreg(0xF804);   // HW_REG_HW_ID
+  const unsigned xcc = __builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
+  return ((((int)(xcc & 7) * 8 + (int)((hw >> 13) & 7)) * 2 + (int)((hw >> 12) & 1)) * 16 +
+          (int)((hw >> 8) & 0xF));
+}
+
+// One bulk task: blocks grp[0 .. G) (-1: none) stepped in lock-step, QL lanes per (block,
+// target), each taking the max-plus chain over IQ sources; G = (64 W) / (QL n).
+template <int W, int QL, int IQ>
 __device__ __forceinline__ void vit_group_task(const SweepArgs& p, unsigned char* smem,
                                                const int32_t* grp, int G, int xr) {
-  constexpr int XB = 2 * IQ2;
+  constexpr int XB = VLds<W, QL, IQ>::XB;
+  constexpr int GM = VLds<W, QL, IQ>::GM;
   constexpr int TB = 64 * W;
   constexpr int TE = 4;     // emission prefetch tile
-  constexpr int NCH = 4;    // independent max chains per lane
-  const int GM = VLds<W, IQ2>::G;
+  constexpr int NCH = 3;    // independent max chains per lane
   double* X = reinterpret_cast<double*>(smem);  // [2][GM][XB]
   double* Y = X + 2 * GM * XB;                  // [GM][XB]
   const int n = p.n;
   const int g = threadIdx.x;
-  const int bq = g / (2 * n);                    // block row of this lane (>= G: idle)
+  const int LB = QL * n;                          // lanes per block
+  const int bq = g / LB;                          // block row of this lane (>= G: idle)
   const bool live = bq < G;
   const int b = live ? bq : 0;
-  const int u = g - bq * 2 * n;
-  const int j = live ? (u >> 1) : 0;             // target state
-  const int q = u & 1;                           // source half
+  const int u = g - bq * LB;
+  const int j = live ? u / QL : 0;                // target state
+  const int q = u % QL;                           // source range
   const int blk = live ? grp[b] : -1;
   const int64_t c0 = blk >= 0 ? p.off[blk] : 0;
   const int T = blk >= 0 ? (int)(p.off[blk + 1] - c0) : 0;
@@ -75,12 +87,12 @@ __device__ __forceinline__ void vit_group_task(const SweepArgs& p, unsigned char
   Tmax = uni(Tmax);
   const int64_t tk0 = blk >= 0 ? p.tile_off[blk] : 0;
 
-  // this lane's half of column j of log a (the diagonal kept out of the chain, see the
-  // VALU Viterbi in valu_sweep.h); sources beyond n read -inf from the padded vector
-  double m[IQ2];
+  // this lane's IQ entries of column j of log a (the diagonal kept out of the chain, see
+  // the VALU Viterbi in valu_sweep.h); sources beyond n read -inf from the padded vector
+  double m[IQ];
 #pragma unroll
-  for (int k = 0; k < IQ2; ++k) {
-    const int i = q * IQ2 + k;
+  for (int k = 0; k < IQ; ++k) {
+    const int i = q * IQ + k;
     m[k] = (act && i < n) ? (i == j ? -INFINITY : p.mat[(int64_t)i * n + j]) : 0.0;
   }
   const double ldiag = act ? p.mat[(int64_t)j * n + j] : 0.0;
@@ -122,19 +134,23 @@ __device__ __forceinline__ void vit_group_task(const SweepArgs& p, unsigned char
       const int t = t0 + sub;
       if (t >= 1 && t < Tmax) {
         const int buf = (t - 1) & 1;
-        const double* xs = X + (buf * GM + b) * XB + q * IQ2;
+        const double* xs = X + (buf * GM + b) * XB + q * IQ;
         // sources in chunks of 8 with scheduling barriers between them, so at most one
         // chunk of the published vector is live in registers beside the slice of log a
         double bc[NCH];
 #pragma unroll
         for (int c = 0; c < NCH; ++c) bc[c] = xs[c] + m[c];
 #pragma unroll
-        for (int k = NCH; k < IQ2; ++k) {
+        for (int k = NCH; k < IQ; ++k) {
           if (k % 8 == 0) __builtin_amdgcn_sched_barrier(0);
           bc[k % NCH] = fmax(bc[k % NCH], xs[k] + m[k]);
         }
-        double zo = fmax(fmax(bc[0], bc[1]), fmax(bc[2], bc[3]));
-        zo = fmax(zo, dpp_f64<0xB1>(zo));  // the other half of the sources (quad_perm 1,0,3,2)
+        double zo = bc[0];
+#pragma unroll
+        for (int c = 1; c < NCH; ++c) zo = fmax(zo, bc[c]);
+        // the other source ranges of this target: the QL lanes of a quad / pair
+        zo = fmax(zo, dpp_f64<0xB1>(zo));                  // quad_perm [1,0,3,2]
+        if constexpr (QL == 4) zo = fmax(zo, dpp_f64<0x4E>(zo));  // quad_perm [2,3,0,1]
         const double ec = ecur[sub % TE];
         const double yd = (x + ldiag) + ec;
         const double yo = zo + ec;
@@ -167,26 +183,42 @@ __device__ __forceinline__ void vit_group_task(const SweepArgs& p, unsigned char
   lds_barrier();
 }
 
-// v.order[0, nurg): the longest blocks as VALU tasks; then groups of G consecutive blocks
-// of v.order[nurg, nblocks)
-template <int W, int IQ2>
-__global__ void __launch_bounds__(64 * W, 1) vit_hybrid_kernel(SweepArgs v, int nurg, int G) {
+// v.order[0, nurg): the longest blocks as VALU tasks (8 lanes per target, IQV sources per
+// lane: the configuration of the VALU-only sweep, so the record stride 8 W matches); then
+// groups of G consecutive blocks of v.order[nurg, nblocks).  A workgroup on a CU whose
+// cu_busy count is positive (another workgroup there decodes a long block) stops pulling
+// bulk work.
+template <int W, int QL, int IQ, int IQV, int WPS>
+__global__ void __launch_bounds__(64 * W, WPS) vit_hybrid_kernel(SweepArgs v, int nurg, int G,
+                                                                 int* cu_busy, int exit_busy) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int qslot[2];
   constexpr int XR = 8 * W;  // record stride: the VALU task's padded targets
   const int64_t nb = v.nblocks;
+  const int key = cu_key();
   for (;;) {
     if (threadIdx.x == 0) qslot[0] = atomicAdd(v.queue, 1);
     lds_barrier();
     const int bi = uni(qslot[0]);
     lds_barrier();
     if (bi >= nurg) break;
-    sweep_task<8, W, 1, (2 * IQ2 + 7) / 8, MODE_VIT>(v, smem, bi);
+    if (threadIdx.x == 0 && exit_busy >= 0) atomicAdd(cu_busy + key, 1);
+    sweep_task<8, W, 1, IQV, MODE_VIT>(v, smem, bi);
+    if (threadIdx.x == 0 && exit_busy >= 0) atomicSub(cu_busy + key, 1);
   }
   __shared__ int32_t grp[16];
   const int64_t ngroups = (nb - nurg + G - 1) / G;
   for (;;) {
-    if (threadIdx.x == 0) qslot[1] = atomicAdd(v.queue + 1, 1);
+    if (threadIdx.x == 0) {
+      // wait (asleep) while a long block is decoded on this CU; exit mode: leave instead
+      while (__hip_atomic_load(cu_busy + key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0) {
+        if (exit_busy) break;
+        __builtin_amdgcn_s_sleep(64);
+      }
+      const bool busy =
+          exit_busy && __hip_atomic_load(cu_busy + key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0;
+      qslot[1] = busy ? (int)ngroups : atomicAdd(v.queue + 1, 1);
+    }
     lds_barrier();
     const int gi = uni(qslot[1]);
     if (gi < ngroups && threadIdx.x < G) {
@@ -195,35 +227,49 @@ __global__ void __launch_bounds__(64 * W, 1) vit_hybrid_kernel(SweepArgs v, int 
     }
     lds_barrier();
     if (gi >= ngroups) break;
-    vit_group_task<W, IQ2>(v, smem, grp, G, XR);
+    vit_group_task<W, QL, IQ>(v, smem, grp, G, XR);
   }
 }
 
 }  // namespace
 
-// Configurations: 12 waves (3 per SIMD: the 36-value slice of log a and the chains fit
-// without spilling); 2*IQ2 >= n, 64W >= 2n (one group of G blocks at least)
+// Configurations (64 < n <= 72): 9 waves (the VALU-only sweep's), record stride 72;
+// cfg 0: four lanes per target, groups of 2 blocks, two workgroups per CU;
+// cfg 1: two lanes per target, groups of 4 blocks, one workgroup per CU
 VitHybridGeometry vit_hybrid_geometry(int n) {
   VitHybridGeometry g{};
   g.cfg = -1;
   if (!getenv("ITR_VIT_HYBRID")) return g;
   if (n > 64 && n <= 72) {
-    g.cfg = 0;
-    g.block = 64 * 12;
-    g.xr = 8 * 12;
-    g.G = (64 * 12) / (2 * n);
-    using V = ValuSweep<8, 12, 1, 9, MODE_VIT>;
-    g.lds = std::max(VLds<12, 36>::bytes, V::lds_bytes);
+    g.cfg = atoi(getenv("ITR_VIT_HYBRID")) == 2 ? 1 : 0;
+    g.exit_busy = getenv("ITR_VIT_EXIT") ? atoi(getenv("ITR_VIT_EXIT")) : 0;
+    if (getenv("ITR_VIT_NOCU")) g.exit_busy = -1;
+    g.block = 64 * 9;
+    g.xr = 8 * 9;
+    using V = ValuSweep<8, 9, 1, 9, MODE_VIT>;
+    if (g.cfg == 0) {
+      g.G = (64 * 9) / (4 * n);
+      g.lds = std::max(VLds<9, 4, 18>::bytes, V::lds_bytes);
+      g.per_cu = 2;
+    } else {
+      g.G = (64 * 9) / (2 * n);
+      g.lds = std::max(VLds<9, 2, 36>::bytes, V::lds_bytes);
+      g.per_cu = 1;
+    }
   }
   return g;
 }
 
 hipError_t launch_vit_hybrid(const VitHybridGeometry& g, int grid, const SweepArgs& v, int nurg,
-                             hipStream_t st) {
+                             int* cu_busy, hipStream_t st) {
   switch (g.cfg) {
     case 0:
-      hipLaunchKernelGGL((vit_hybrid_kernel<12, 36>), dim3(grid), dim3(g.block), g.lds, st, v,
-                         nurg, g.G);
+      hipLaunchKernelGGL((vit_hybrid_kernel<9, 4, 18, 9, 6>), dim3(grid), dim3(g.block), g.lds,
+                         st, v, nurg, g.G, cu_busy, g.exit_busy);
+      break;
+    case 1:
+      hipLaunchKernelGGL((vit_hybrid_kernel<9, 2, 36, 9, 3>), dim3(grid), dim3(g.block), g.lds,
+                         st, v, nurg, g.G, cu_busy, g.exit_busy);
       break;
     default: return hipErrorInvalidValue;
   }
@@ -236,7 +282,8 @@ VitHybridGeometry vit_hybrid_geometry(int) {
   g.cfg = -1;
   return g;
 }
-hipError_t launch_vit_hybrid(const VitHybridGeometry&, int, const SweepArgs&, int, hipStream_t) {
+hipError_t launch_vit_hybrid(const VitHybridGeometry&, int, const SweepArgs&, int, int*,
+                             hipStream_t) {
   return hipErrorInvalidValue;
 }
 #endif

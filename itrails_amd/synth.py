@@ -118,3 +118,30 @@ def sample_alignment_range(a, b, pi, lengths, lo: int, hi: int, seed: int = 0,
     off = np.zeros(hi - lo + 1, dtype=np.int64)
     np.cumsum(lengths[lo:hi], out=off[1:])
     return np.concatenate(parts), off
+
+
+def write_maf(path, obs, off, species, seed: int = 0, p_gap_of_n: float = 0.5,
+              chrom_size: int = 250_000_000):
+    """Write symbols (obs / off, the 625-letter alphabet of read_data.py:6-24) as a MAF file
+    that maf_parser reads back to the same symbols: one alignment block per block, the four
+    species in `species` order, every N written as '-' with probability p_gap_of_n (the
+    reader maps '-' to N, read_data.py:106), blocks placed one after another on the first
+    species' chromosome (+ strand) so parse_coordinates gives positions with -9 at its gaps."""
+    rng = np.random.default_rng(seed)
+    names = np.array([list(s) for s in get_obs_state_dct()])  # 625 x 4 letters
+    pos = 10_000
+    with open(path, "w") as f:
+        f.write("##maf version=1 scoring=synthetic\n\n")
+        for k in range(len(off) - 1):
+            cols = names[np.asarray(obs[off[k]:off[k + 1]], dtype=np.int64)]  # T x 4
+            if len(cols) == 0:
+                continue
+            gap = (cols == "N") & (rng.random(cols.shape) < p_gap_of_n)
+            cols = np.where(gap, "-", cols)
+            f.write("a score=0.0\n")
+            for s, name in enumerate(species):
+                seq = "".join(cols[:, s])
+                size = len(seq) - seq.count("-")
+                f.write(f"s {name}.chr1 {pos} {size} + {chrom_size} {seq}\n")
+            f.write("\n")
+            pos += len(cols) + 100

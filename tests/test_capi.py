@@ -16,6 +16,19 @@ def test_library_exports_every_header_symbol():
     assert set(syms) == set(_lib._SIGNATURES), "ctypes signatures out of sync with header"
 
 
+def test_one_hip_runtime_when_library_loads_first():
+    """Loading the library before anything imports torch must not map a second HIP runtime
+    next to torch's (two runtimes in one process: the second finds no device)."""
+    import subprocess
+    import sys
+    code = ("import itrails_amd._lib as L; L.lib(); import torch; "
+            "m = open('/proc/self/maps').read(); "
+            "print(len({l.split()[-1] for l in m.splitlines() if 'libamdhip64' in l}))")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         check=True, cwd=_lib.os.path.dirname(_lib.HERE))
+    assert out.stdout.strip().splitlines()[-1] == "1"
+
+
 def test_version_and_argument_errors():
     L = _lib.lib()
     assert L.itr_version() == 1

@@ -347,3 +347,39 @@ def test_optimize_cli_runs(gpu, maf_case):
     lls = [float(r.split(",")[-2]) for r in hist[1:]]
     assert best["results"]["log_likelihood"] == max(lls)
     assert set(best["optimized_parameters"]) == {"t_1", "N_ABC", "t_upper"}
+
+
+@pytest.mark.gpu
+def test_viterbi_cli_config1(gpu, tmp_path):
+    """BASELINE config 1 through the drop-in CLI: itrails-viterbi on a synthetic 100 kbp
+    (5,5) MAF (gaps and Ns, reference coordinates), viterbi.csv byte-identical to the file
+    written from the CPU restatement's paths on the same model and the same parsed input."""
+    from itrails_amd.cli import viterbi_main
+    from itrails_amd.maf import read_maf
+    from itrails_amd.synth import block_lengths, sample_alignment, write_maf
+    from itrails_amd.tables import build_tables
+    from itrails_amd.writers import write_viterbi_csv
+    from oracle import hmm_oracle as O
+    from conftest import golden
+
+    g = golden("model_kat_5_5.npz")
+    lengths = block_lengths(np.random.default_rng(21), 100_000, 2000.0)
+    obs, off, _ = sample_alignment(g["a"], g["b"], g["pi"], lengths, seed=22)
+    maf = tmp_path / "chr.maf"
+    write_maf(str(maf), obs, off, SP, seed=23)
+    cfg = _decode_config(tmp_path, settings__n_int_AB=5, settings__n_int_ABC=5,
+                         settings__input_maf=str(maf))
+    cfg["settings"]["reference"] = "hg38"
+    cf = tmp_path / "cfg.yaml"
+    yaml.dump(cfg, open(cf, "w"))
+    viterbi_main(["--config-file", str(cf), "--output", str(tmp_path / "v" / "x")])
+    s = C.resolve_decode(yaml.safe_load(open(cf)), output_cmd=str(tmp_path / "chk" / "x"))
+    a, b, pi, _, _ = _model_from_setup(s)
+    robs, roff, coords, _ = read_maf(str(maf), SP, "hg38")
+    assert np.array_equal(robs, obs) and np.array_equal(roff, off)
+    ref_path = O.viterbi(build_tables(a, b, pi), robs, roff)
+    write_viterbi_csv(str(tmp_path / "expect.csv"), ref_path.astype(np.uint8),
+                      ref_coordinates=coords, block_off=roff)
+    got = open(tmp_path / "v" / "x.viterbi.csv").read()
+    assert got == open(tmp_path / "expect.csv").read()
+    assert got.count("\n") > len(lengths)  # segments with coordinates, every block present
