@@ -163,6 +163,22 @@ ITR_API int itr_expm_batched_host(int n, int64_t batch, const double* h_A, doubl
 ITR_API int itr_expm_blocktri_batched(int n_block, int n_blocks, int64_t batch,
                                       const double* d_A, double* d_out, void* stream);
 
+/* Van Loan integrals of many omega paths at once (vanloan.py:392-425): for path p with
+ * mask ids w_0 .. w_{L-1} (h_path_mask[h_path_off[p] .. h_path_off[p+1]), L >= 1) on interval
+ * h_path_job[p] of length t = h_t[job], d_out[p] (n x n) = expm(C_p t)[0:n, -n:] with C_p
+ * block bidiagonal: diagonal blocks h_Q (n x n), super-diagonal blocks
+ * diag(m_{w_i}) h_Q diag(m_{w_{i+1}}), m_w = h_masks[w*n .. w*n+n) (0/1 bytes).  A path of
+ * length 1 gives expm(Q t).  Every block of every Pade intermediate is formed once per
+ * distinct (interval, sub-path) and shared by all paths containing it (vanloan.hip); one
+ * Pade branch and scaling per interval, from the largest ||C_p t||_1 of its paths
+ * (expm.py:16-143).  Host arrays are read before the call returns; the work is queued on
+ * `stream` without host synchronisation.  Replaces the per-path vanloan calls of
+ * run_markov_chain_ABC.py:407-490 (and the Van Loan integrals of the introgression chains). */
+ITR_API int itr_vanloan_paths(int n, const double* h_Q, int n_jobs, const double* h_t,
+                              int n_masks, const uint8_t* h_masks, int64_t n_paths,
+                              const int32_t* h_path_job, const int64_t* h_path_off,
+                              const int32_t* h_path_mask, double* d_out, void* stream);
+
 /* Solve M_b X_b = R_b for b < batch (M n x n, R n x nrhs, row-major, contiguous batches).
  * M is overwritten by its LU factors (partial pivoting, first maximum |.| like LAPACK
  * idamax), R by X.  Replaces np.linalg.inv in deepest_ti (deepest_ti.py:256: the last n

@@ -860,6 +860,7 @@ int itr_posterior_host(itr_model_t m, itr_plan_t p, const uint16_t* h_obs, doubl
 
 int itr_release_staging(void) {
   g_stage.release();
+  itr::release_vanloan_workspace();
   return 0;
 }
 
@@ -908,6 +909,39 @@ int itr_expm_blocktri_batched(int n_block, int n_blocks, int64_t batch, const do
   Scope sc("expm", st);
   const hipError_t e = itr::expm_blocktri_batched(n_block, n_blocks, batch, A, out, st);
   if (e != hipSuccess) return fail(ITR_EHIP, "block expm failed: %s", hipGetErrorString(e));
+  return 0;
+}
+
+int itr_vanloan_paths(int n, const double* h_Q, int n_jobs, const double* h_t, int n_masks,
+                      const uint8_t* h_masks, int64_t n_paths, const int32_t* h_path_job,
+                      const int64_t* h_path_off, const int32_t* h_path_mask, double* d_out,
+                      void* stream) {
+  if (n < 1 || n_jobs < 0 || n_masks < 0 || n_paths < 0)
+    return fail(ITR_EINVAL, "bad Van Loan shape n=%d jobs=%d masks=%d paths=%lld", n, n_jobs,
+                n_masks, (long long)n_paths);
+  if (n_paths == 0) return 0;
+  if (!h_Q || !h_t || !h_path_job || !h_path_off || !h_path_mask || !d_out)
+    return fail(ITR_EINVAL, "null pointer");
+  if (h_path_off[0] != 0) return fail(ITR_EINVAL, "path offsets must start at 0");
+  for (int64_t p = 0; p < n_paths; ++p) {
+    const int64_t L = h_path_off[p + 1] - h_path_off[p];
+    if (L < 1) return fail(ITR_EINVAL, "path %lld is empty", (long long)p);
+    if (h_path_job[p] < 0 || h_path_job[p] >= n_jobs)
+      return fail(ITR_EINVAL, "path %lld: interval %d out of range", (long long)p,
+                  h_path_job[p]);
+    if (L > 1)
+      for (int64_t i = h_path_off[p]; i < h_path_off[p + 1]; ++i)
+        if (h_path_mask[i] < 0 || h_path_mask[i] >= n_masks)
+          return fail(ITR_EINVAL, "path %lld: mask id %d out of range", (long long)p,
+                      h_path_mask[i]);
+  }
+  if (n_masks > 0 && !h_masks) return fail(ITR_EINVAL, "null masks");
+  hipStream_t st = (hipStream_t)stream;
+  Scope sc("vanloan", st);
+  const hipError_t e = itr::vanloan_paths(n, h_Q, n_jobs, h_t, n_masks, h_masks, n_paths,
+                                          h_path_job, h_path_off, h_path_mask, d_out, st);
+  if (e != hipSuccess) return fail(ITR_EHIP, "Van Loan evaluation failed: %s",
+                                   hipGetErrorString(e));
   return 0;
 }
 

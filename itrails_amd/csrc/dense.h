@@ -38,6 +38,14 @@ hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipS
 hipError_t expm_blocktri_batched(int nb, int kb, int64_t batch, const double* A, double* out,
                                  hipStream_t st);
 
+// Van Loan integrals of many omega paths, shared sub-path evaluation (vanloan.hip; the
+// arguments of itr_vanloan_paths)
+hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t, int nmasks,
+                         const uint8_t* h_masks, int64_t npaths, const int32_t* h_job,
+                         const int64_t* h_off, const int32_t* h_mask, double* d_out,
+                         hipStream_t st);
+void release_vanloan_workspace();
+
 // emission rows (emission.hip): tables [n_states x 512] -> out [n_states x 256]
 hipError_t launch_emission(int n_states, const double* tables, double* out, hipStream_t st);
 

@@ -264,7 +264,7 @@ hipError_t launch_vit_hybrid(const VitHybridGeometry& g, int grid, const SweepAr
                              int* cu_busy, hipStream_t st) {
   switch (g.cfg) {
     case 0:
-      hipLaunchKernelGGL((vit_hybrid_kernel<9, 4, 18, 9, 6>), dim3(grid), dim3(g.block), g.lds,
+      hipLaunchKernelGGL((vit_hybrid_kernel<9, 4, 18, 9, 5>), dim3(grid), dim3(g.block), g.lds,
                          st, v, nurg, g.G, cu_busy, g.exit_busy);
       break;
     case 1:

@@ -18,7 +18,8 @@ import numpy as np
 
 from ._lib import check, lib
 
-__all__ = ["expm", "expm_batched", "expm_blocktri_batched", "solve_batched", "gemm_batched"]
+__all__ = ["expm", "expm_batched", "expm_blocktri_batched", "vanloan_paths", "solve_batched",
+           "gemm_batched"]
 
 
 def _dev(x):
@@ -61,6 +62,35 @@ def expm_blocktri_batched(A, n_blocks: int):
         check(lib().itr_expm_blocktri_batched(d.shape[1] // n_blocks, n_blocks, d.shape[0],
                                               d.data_ptr(), out.data_ptr(), _stream()))
     return out if on_dev else out.cpu().numpy()
+
+
+def vanloan_paths(Q, t, masks_u8, path_job, path_off, path_mask):
+    """Van Loan integrals of many omega paths in one shared evaluation (itr_vanloan_paths):
+    returns a torch.cuda (n_paths, n, n) tensor, entry p = expm(C_p t[path_job[p]])[:n, -n:]
+    with C_p the block bidiagonal matrix of vanloan.py:392-425 for the mask ids
+    path_mask[path_off[p]:path_off[p+1]] (a length-1 path gives expm(Q t)).  Q, t, masks and
+    the path arrays are host NumPy arrays; nothing is synchronised."""
+    import torch
+    Q = np.ascontiguousarray(Q, dtype=np.float64)
+    t = np.ascontiguousarray(t, dtype=np.float64)
+    masks_u8 = np.ascontiguousarray(masks_u8, dtype=np.uint8)
+    path_job = np.ascontiguousarray(path_job, dtype=np.int32)
+    path_off = np.ascontiguousarray(path_off, dtype=np.int64)
+    path_mask = np.ascontiguousarray(path_mask, dtype=np.int32)
+    n = Q.shape[0]
+    if Q.ndim != 2 or Q.shape[1] != n or masks_u8.ndim != 2 or \
+            (masks_u8.size and masks_u8.shape[1] != n):
+        raise ValueError("expected Q (n, n) and masks (n_masks, n)")
+    npaths = len(path_job)
+    if len(path_off) != npaths + 1:
+        raise ValueError("path_off must have n_paths + 1 entries")
+    out = torch.empty((npaths, n, n), dtype=torch.float64, device="cuda")
+    if npaths:
+        check(lib().itr_vanloan_paths(n, Q.ctypes.data, len(t), t.ctypes.data,
+                                      masks_u8.shape[0], masks_u8.ctypes.data, npaths,
+                                      path_job.ctypes.data, path_off.ctypes.data,
+                                      path_mask.ctypes.data, out.data_ptr(), _stream()))
+    return out
 
 
 def expm(A):

@@ -122,6 +122,8 @@ def run_chain_abc(Q, times, ss, probs: Dict, n_int, la) -> Dict:
     plan = _abc_plan(n_int, tuple(probs.keys()))
     if plan is None:  # an interval whose path-by-path order matters: the dict form
         return _run_chain_abc_dicts(Q, times, ss, probs, n_int, la)
+    if hasattr(la, "vanloan_batch"):
+        return _run_chain_abc_device(plan, Q, times, ss, probs, la)
     return _run_chain_abc_planned(plan, Q, times, ss, probs, la)
 
 
@@ -220,7 +222,7 @@ class _IntervalPlan:
 
 class _ABCPlan:
     __slots__ = ("nrows", "omegas", "intervals", "close_paths", "close_order", "close_groups",
-                 "close_sum_rows")
+                 "close_sum_rows", "dev")
 
 
 @lru_cache(maxsize=16)
@@ -362,6 +364,7 @@ def _abc_plan(n_int: int, keys0: tuple):
                           np.asarray(ts, dtype=np.int64),
                           np.asarray([task_rows[t] for t in ts], dtype=np.int64))
                          for sub, ts in cg.items()]
+    plan.dev = {}
     return plan
 
 
@@ -404,6 +407,166 @@ def _run_chain_abc_planned(plan, Q, times, ss, probs: Dict, la) -> Dict:
     out: Dict = {}
     for key, kind, k in plan.close_order:
         out[key] = float(sums[k]) if kind == "sum" else float(deep[k])
+    return out
+
+
+class _DevInterval:
+    __slots__ = ("e_idx", "vl0", "vl1", "plain", "ng", "sum_steps", "rows", "rmax")
+
+
+def _group_tables(dev, pids_list, rows_of_group):
+    """Index tensors of a set of path groups: the sequential sum steps of each group's
+    matrix (step k adds the k-th path of every group that has one: the reference's
+    left-to-right S = S_0 + S_1 + ..., run_markov_chain_ABC.py:478-486) and, for the row
+    products, every row's (group, slot) in a zero-padded [groups, rmax] layout."""
+    import torch
+    steps = []
+    kmax = max((len(p) for p in pids_list), default=0)
+    for k in range(kmax):
+        gs = [g for g, p in enumerate(pids_list) if len(p) > k]
+        ps = [int(pids_list[g][k]) for g in gs]
+        steps.append((torch.as_tensor(gs, dtype=torch.long, device=dev),
+                      torch.as_tensor(ps, dtype=torch.long, device=dev)))
+    gid, slot = [], []
+    rmax = 0
+    for g, rows in enumerate(rows_of_group):
+        for k in range(rows):
+            gid.append(g)
+            slot.append(k)
+        rmax = max(rmax, rows)
+    return steps, (torch.as_tensor(gid, dtype=torch.long, device=dev),
+                   torch.as_tensor(slot, dtype=torch.long, device=dev)), rmax
+
+
+def _device_tables(plan, Q, ss, la):
+    """Per-device constant tables of a plan (built on first use, reused by every rebuild):
+    the Van Loan path arrays of all intervals (one itr_vanloan_paths call per rebuild: jobs
+    0 .. I-1 the Van Loan paths of interval i, jobs I .. 2I-1 the interval propagator
+    expm(Q dt_i) as a length-1 path), the omega mask rows and every row index as device
+    tensors."""
+    import torch
+    masks = ss.omega_masks
+    key = (str(la.dev), tuple(masks))
+    if key in plan.dev:
+        return plan.dev[key]
+    dev = la.dev
+    n = Q.shape[0]
+    keys = list(masks)
+    mid = {k: i for i, k in enumerate(keys)}
+    I = len(plan.intervals)
+    job, lens, pm = [], [], []
+    ivs = []
+    for i, ip in enumerate(plan.intervals):
+        d = _DevInterval()
+        d.vl0 = len(job)
+        for p in ip.vl_paths:
+            job.append(i)
+            lens.append(len(p))
+            pm.extend(mid[w] for w in p)
+        d.vl1 = len(job)
+        ivs.append(d)
+    for i, d in enumerate(ivs):
+        d.e_idx = len(job)
+        job.append(I + i)
+        lens.append(1)
+        pm.append(0)
+    off = np.zeros(len(job) + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    T = lambda a: torch.as_tensor(np.asarray(a, dtype=np.int64), device=dev)  # noqa: E731
+    for d, ip in zip(ivs, plan.intervals):
+        src, oms, ome, dst = ip.plain
+        d.plain = (T(src), T(oms), T(ome), T(dst)) if src.size else None
+        d.ng = len(ip.groups)
+        pids_list = [g[0] for g in ip.groups]
+        d.sum_steps, (gid, slot), d.rmax = _group_tables(dev, pids_list,
+                                                         [g[1].size for g in ip.groups])
+        if d.ng:
+            cat = lambda j: np.concatenate([g[j] for g in ip.groups])  # noqa: E731
+            d.rows = (T(cat(1)), T(cat(2)), T(cat(3)), T(cat(4)), gid, slot)
+        else:
+            d.rows = None
+    tab = {
+        "mask_u8": np.stack([np.asarray(masks[k], dtype=np.uint8) for k in keys]),
+        "job": np.asarray(job, dtype=np.int32), "off": off,
+        "pm": np.asarray(pm, dtype=np.int32), "ivs": ivs,
+        "F": torch.as_tensor(np.stack([masks[om].astype(np.float64) for om in plan.omegas])
+                             if plan.omegas else np.zeros((0, n)), device=dev),
+    }
+    absorbing = (7, 7)
+    keep = ~masks[absorbing]
+    tab["keep"] = torch.as_tensor(np.nonzero(keep)[0], dtype=torch.long, device=dev)
+    tab["sum_rows"] = T(plan.close_sum_rows)
+    cpids = [g[0] for g in plan.close_groups]
+    tab["c_steps"], (cg, cs), tab["c_rmax"] = _group_tables(
+        dev, cpids, [g[2].size for g in plan.close_groups])
+    if plan.close_groups:
+        tab["c_rows"] = (T(np.concatenate([g[2] for g in plan.close_groups])), cg, cs,
+                         T(np.concatenate([g[1] for g in plan.close_groups])))
+    tab["ntasks"] = sum(len(t) for _, t, _ in plan.close_groups)
+    plan.dev[key] = tab
+    return tab
+
+
+def _group_matrices(S, steps, ng, n):
+    """M[g] = S[p_g0] + S[p_g1] + ... in path order (see _group_tables)."""
+    import torch
+    M = torch.zeros((ng, n, n), dtype=S.dtype, device=S.device)
+    for gs, ps in steps:
+        M[gs] += S[ps]
+    return M
+
+
+def _run_chain_abc_device(plan, Q, times, ss, probs: Dict, la) -> Dict:
+    """_run_chain_abc_planned with every number resident on the device: one shared Van Loan
+    evaluation for all intervals (their propagators included), the key rows as one
+    [rows, n] tensor advanced interval by interval, the closing phase's contractions; a
+    single device-to-host copy of the final per-key probabilities."""
+    import torch
+    tab = _device_tables(plan, Q, ss, la)
+    masks = ss.omega_masks
+    n = Q.shape[0]
+    dev = la.dev
+    I = len(plan.intervals)
+    t = np.asarray([times[i] for i in range(I)] * 2, dtype=np.float64)
+    S_all = la.vanloan_batch(Q, tab["mask_u8"], t, tab["job"], tab["off"], tab["pm"])
+    F = tab["F"]
+    P = torch.zeros((plan.nrows, n), dtype=torch.float64, device=dev)
+    P0 = np.zeros((len(probs), n))
+    for i, v in enumerate(probs.values()):
+        P0[i] = v[0]
+    P[:len(probs)] = torch.from_numpy(P0).to(dev)
+    for d in tab["ivs"]:
+        Pn = P.clone()
+        if d.plain is not None:
+            src, oms, ome, dst = d.plain
+            Pn[dst] = ((P[src] * F[oms]) @ S_all[d.e_idx]) * F[ome]
+        if d.rows is not None:
+            src, oms, ome, dst, gid, slot = d.rows
+            M = _group_matrices(S_all[d.vl0:d.vl1], d.sum_steps, d.ng, n)
+            V = torch.zeros((d.ng, d.rmax, n), dtype=torch.float64, device=dev)
+            V[gid, slot] = P[src] * F[oms]
+            Pn[dst] = torch.bmm(V, M)[gid, slot] * F[ome]
+        P = Pn
+    absorbing = (7, 7)
+    keep = tab["keep"]
+    Qn = Q[~masks[absorbing]][:, ~masks[absorbing]]
+    sums = P[tab["sum_rows"]].sum(dim=1) if plan.close_sum_rows.size else \
+        torch.zeros(0, dtype=torch.float64, device=dev)
+    deep = torch.zeros(tab["ntasks"], dtype=torch.float64, device=dev)
+    if plan.close_paths:
+        D = la.deepest_t(Qn, masks_without(masks, absorbing), plan.close_paths)
+        rws, gid, slot, tasks = tab["c_rows"]
+        ng = len(plan.close_groups)
+        nk = keep.numel()
+        M = _group_matrices(D, tab["c_steps"], ng, nk)
+        V = torch.zeros((ng, tab["c_rmax"], nk), dtype=torch.float64, device=dev)
+        V[gid, slot] = P[rws][:, keep]
+        deep[tasks] = torch.bmm(V, M)[gid, slot].sum(dim=1)
+    host = torch.cat([sums, deep]).cpu().numpy()
+    ns = sums.numel()
+    out: Dict = {}
+    for key, kind, k in plan.close_order:
+        out[key] = float(host[k]) if kind == "sum" else float(host[ns + k])
     return out
 
 

@@ -66,34 +66,24 @@ class DeviceLinalg:
             C[:, (blk - 1) * n:blk * n, blk * n:(blk + 1) * n] = A
         return C
 
-    def vanloan(self, Q: np.ndarray, t: float, masks: Dict[Omega, np.ndarray],
-                paths: Sequence[Tuple[Omega, ...]]) -> List[np.ndarray]:
-        """expm(C t)[:n, -n:] for each omega path (vanloan.py:392-425); C is block upper
-        bidiagonal with Q on the diagonal, so the block-triangular expm forms only the upper
-        blocks."""
-        from ..dense import expm_blocktri_batched
-        n = Q.shape[0]
-        out: List[np.ndarray] = [None] * len(paths)
-        by_len: Dict[int, List[int]] = {}
-        for i, p in enumerate(paths):
-            by_len.setdefault(len(p), []).append(i)
-        for L, idx in sorted(by_len.items()):
-            C = self._block_matrices(Q, masks, [paths[i] for i in idx], L, float(t), L)
-            E = expm_blocktri_batched(C, L)[:, :n, -n:].cpu().numpy()
-            for k, i in enumerate(idx):
-                out[i] = E[k]
-        self.stats["vanloan"] += len(paths)
-        return out
+    # ---- device-resident forms (torch.cuda tensors out; used by the planned chains) -----
+    def vanloan_batch(self, Q: np.ndarray, masks_u8: np.ndarray, t: np.ndarray,
+                      path_job: np.ndarray, path_off: np.ndarray, path_mask: np.ndarray):
+        """(n_paths, n, n) device tensor of Van Loan integrals over several intervals at once
+        (dense.vanloan_paths: shared sub-path evaluation, vanloan.hip)."""
+        from ..dense import vanloan_paths
+        self.stats["vanloan"] += len(path_job)
+        return vanloan_paths(Q, t, masks_u8, path_job, path_off, path_mask)
 
-    def deepest(self, Q: np.ndarray, masks: Dict[Omega, np.ndarray],
-                paths: Sequence[Tuple[Omega, ...]]) -> List[np.ndarray]:
-        """(-C^-1)[:n, -n:] @ (diag(m p[-2]) Q diag(m p[-1])) for each omega path
-        (deepest_ti.py:215-256); the last n columns of C^-1 come from one batched solve
-        against the last n columns of the identity."""
-        from ..dense import solve_batched
+    def deepest_t(self, Q: np.ndarray, masks: Dict[Omega, np.ndarray],
+                  paths: Sequence[Tuple[Omega, ...]]):
+        """(n_paths, n, n) device tensor: (-C^-1)[:n, -n:] @ (diag(m p[-2]) Q diag(m p[-1]))
+        for each omega path (deepest_ti.py:215-256); the last n columns of C^-1 come from one
+        batched solve against the last n columns of the identity, per path length."""
+        from ..dense import gemm_batched, solve_batched
         torch = self.torch
         n = Q.shape[0]
-        out: List[np.ndarray] = [None] * len(paths)
+        out = torch.empty((len(paths), n, n), dtype=torch.float64, device=self.dev)
         by_len: Dict[int, List[int]] = {}
         for i, p in enumerate(paths):
             by_len.setdefault(len(p), []).append(i)
@@ -109,12 +99,34 @@ class DeviceLinalg:
             ma = torch.from_numpy(np.stack([masks[p[-2]] for p in sub]).astype(np.float64)).to(self.dev)
             mb = torch.from_numpy(np.stack([masks[p[-1]] for p in sub]).astype(np.float64)).to(self.dev)
             A = (ma[:, :, None] * dQ[None] * mb[:, None, :]).contiguous()
-            from ..dense import gemm_batched
-            D = gemm_batched(X.contiguous(), A, alpha=-1.0).cpu().numpy()
-            for k, i in enumerate(idx):
-                out[i] = D[k]
+            out[torch.as_tensor(idx, device=self.dev)] = gemm_batched(X.contiguous(), A,
+                                                                      alpha=-1.0)
         self.stats["deepest"] += len(paths)
         return out
+
+    # ---- host-array forms (the dictionary chains, the introgression model) ---------------
+    def vanloan(self, Q: np.ndarray, t: float, masks: Dict[Omega, np.ndarray],
+                paths: Sequence[Tuple[Omega, ...]]) -> List[np.ndarray]:
+        """expm(C t)[:n, -n:] for each omega path (vanloan.py:392-425), one shared
+        evaluation of all paths (vanloan.hip)."""
+        if not len(paths):
+            return []
+        keys = list(masks)
+        mid = {k: i for i, k in enumerate(keys)}
+        mu8 = np.stack([np.asarray(masks[k], dtype=np.uint8) for k in keys])
+        off = np.zeros(len(paths) + 1, dtype=np.int64)
+        np.cumsum([len(p) for p in paths], out=off[1:])
+        pm = np.asarray([mid[w] for p in paths for w in p], dtype=np.int32)
+        S = self.vanloan_batch(Q, mu8, np.asarray([t], dtype=np.float64),
+                               np.zeros(len(paths), dtype=np.int32), off, pm).cpu().numpy()
+        return list(S)
+
+    def deepest(self, Q: np.ndarray, masks: Dict[Omega, np.ndarray],
+                paths: Sequence[Tuple[Omega, ...]]) -> List[np.ndarray]:
+        """deepest_t as host arrays."""
+        if not len(paths):
+            return []
+        return list(self.deepest_t(Q, masks, paths).cpu().numpy())
 
     def rowmat(self, V: np.ndarray, M: np.ndarray) -> np.ndarray:
         """V @ M for a stack of row vectors V (k x n) and one n x n propagator: the per-key

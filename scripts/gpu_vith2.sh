@@ -27,3 +27,5 @@ for f in 0.25 0.4; do
   run "ql2_wait_$f" ITR_VIT_HYBRID=2 ITR_VIT_URGENT_FRAC=$f || exit 1
 done
 cat gpurun_out/vith2.log
+timeout -k 10 300 python -u scripts/prof_build.py 5 4 > gpurun_out/prof_build.log 2>&1 || { tail -20 gpurun_out/prof_build.log; exit 1; }
+head -5 gpurun_out/prof_build.log

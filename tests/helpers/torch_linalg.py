@@ -1,0 +1,67 @@
+"""Stand-ins for checking the device-resident form of the planned three-species chain
+(chains._run_chain_abc_device: one Van Loan batch for all intervals, key rows as one tensor,
+group sums in path order, padded batched row products, closing contractions) on the CPU —
+TEST INFRASTRUCTURE ONLY.
+
+The two fakes return the same deterministic pseudo-random matrices for every Van Loan /
+deepest-interval request (seeded by the path's mask rows and the interval length), one as
+NumPy lists for the host form (_run_chain_abc_planned), one as torch CPU tensors for the
+device form.  Equal chain outputs then show that the device form routes every row, group,
+sum and overwrite exactly like the host form; the matrix functions themselves are checked on
+the GPU against the reference's models."""
+import hashlib
+
+import numpy as np
+import torch
+
+from helpers.np_linalg import NumpyLinalg
+
+
+def _fake(n, rows, t):
+    h = hashlib.sha256(b"".join(r.tobytes() for r in rows) + np.float64(t).tobytes())
+    rng = np.random.default_rng(int.from_bytes(h.digest()[:8], "little"))
+    return rng.random((n, n)) * 1e-2
+
+
+class FakeNumpyLinalg(NumpyLinalg):
+    def vanloan(self, Q, t, masks, paths):
+        self.stats["vanloan"] += len(paths)
+        n = Q.shape[0]
+        return [_fake(n, [np.asarray(masks[w], dtype=np.uint8) for w in p] if len(p) > 1
+                      else [], t) for p in paths]
+
+    def deepest(self, Q, masks, paths):
+        self.stats["deepest"] += len(paths)
+        n = Q.shape[0]
+        return [_fake(n, [np.asarray(masks[w], dtype=np.uint8) for w in p], -1.0)
+                for p in paths]
+
+    def expm(self, mats):  # interval propagators: a length-1 "path"
+        self.stats["expm"] += len(mats)
+        return [_fake(m.shape[0], [], float(np.abs(m).sum())) if m.shape[0] > 100
+                else super(FakeNumpyLinalg, self).expm([m])[0] for m in mats]
+
+
+class FakeTorchLinalg(FakeNumpyLinalg):
+    dev = torch.device("cpu")
+
+    def vanloan_batch(self, Q, masks_u8, t, path_job, path_off, path_mask):
+        n = Q.shape[0]
+        out = []
+        I = len(t) // 2
+        for p in range(len(path_job)):
+            ids = path_mask[path_off[p]:path_off[p + 1]]
+            j = int(path_job[p])
+            if j >= I:  # the propagator job of interval j - I: what expm() above returns
+                out.append(_fake(n, [], float(np.abs(Q * t[j]).sum())))
+            else:
+                out.append(_fake(n, [masks_u8[i] for i in ids] if len(ids) > 1 else [], t[j]))
+        self.stats["vanloan"] += len(path_job)
+        return torch.from_numpy(np.stack(out)) if out else torch.zeros((0, n, n),
+                                                                       dtype=torch.float64)
+
+    def deepest_t(self, Q, masks, paths):
+        n = Q.shape[0]
+        D = self.deepest(Q, masks, paths)
+        return torch.from_numpy(np.stack(D)) if D else torch.zeros((0, n, n),
+                                                                   dtype=torch.float64)

@@ -108,3 +108,41 @@ def test_expm_blocktri_matches_dense(gpu, n, k):
                 scale = max(np.abs(ref[blk]).max(), 1e-300)
                 assert np.abs(B[b][blk] - D[b][blk]).max() <= 1e-12 * max(scale, 1.0)
                 assert np.abs(B[b][blk] - ref[blk]).max() <= 1e-11 * max(scale, 1.0)
+
+
+@pytest.mark.parametrize("n,nmask", [(5, 3), (17, 4), (70, 6), (203, 9)])
+def test_vanloan_paths_shared_matches_per_path(gpu, n, nmask):
+    """itr_vanloan_paths (shared sub-path evaluation, one Pade branch and scaling per
+    interval) against scipy's expm of each path's block matrix: paths of length 1..5 that
+    share prefixes and suffixes, three intervals whose norms select different branches and
+    squaring counts, duplicates and interleaved intervals in the request order."""
+    import scipy.linalg as sl
+    from itrails_amd.dense import vanloan_paths
+    rng = np.random.default_rng(n + 1000 * nmask)
+    Q = rng.random((n, n)) * (rng.random((n, n)) < 0.3)
+    np.fill_diagonal(Q, 0.0)
+    np.fill_diagonal(Q, -Q.sum(axis=1))
+    Q /= max(1.0, np.abs(Q).sum(axis=0).max())  # ||Q||_1 <= 1
+    masks = (rng.random((nmask, n)) < 0.5).astype(np.uint8)
+    t = np.array([0.02, 0.6, 9.0])  # Pade 5-7, 9-13 without / with squarings
+    paths = []
+    for _ in range(40):
+        L = int(rng.integers(1, 6))
+        paths.append((int(rng.integers(0, 3)), [int(x) for x in rng.integers(0, nmask, L)]))
+    paths += [paths[3], (paths[5][0], paths[5][1][:2]), (2, [0]), (0, [1, 2, 1, 2, 1])]
+    job = np.array([j for j, _ in paths], dtype=np.int32)
+    off = np.zeros(len(paths) + 1, dtype=np.int64)
+    np.cumsum([len(p) for _, p in paths], out=off[1:])
+    pm = np.array([w for _, p in paths for w in p], dtype=np.int32)
+    got = vanloan_paths(Q, t, masks, job, off, pm).cpu().numpy()
+    for k, (j, p) in enumerate(paths):
+        L = len(p)
+        C = np.zeros((n * L, n * L))
+        for b in range(L):
+            C[b * n:(b + 1) * n, b * n:(b + 1) * n] = Q
+        for b in range(1, L):
+            C[(b - 1) * n:b * n, b * n:(b + 1) * n] = masks[p[b - 1]][:, None] * Q * \
+                masks[p[b]][None, :]
+        ref = sl.expm(C * t[j])[:n, -n:]
+        scale = max(np.abs(ref).max(), 1e-300)
+        assert np.abs(got[k] - ref).max() <= 1e-11 * max(scale, 1.0), (k, j, L)

@@ -68,3 +68,19 @@ def test_model_bookkeeping_on_host_backend(name):
     assert np.allclose(a, g["a"], rtol=1e-10, atol=1e-15)
     assert np.allclose(pi, g["pi"], rtol=1e-10, atol=1e-15)
     assert np.allclose(b, g["b"], rtol=1e-8, atol=1e-15)
+
+
+@pytest.mark.parametrize("name", ["model_kat_3_3.npz"])
+def test_device_chain_routes_like_host_chain(name):
+    """The device-resident planned chain (torch tensors) and the host planned chain (NumPy)
+    fed the same deterministic stand-in matrix functions give the same model: every row,
+    group sum, overwrite and closing contraction is routed identically (helpers/torch_linalg)."""
+    from helpers.torch_linalg import FakeNumpyLinalg, FakeTorchLinalg
+    from itrails_amd.model import trans_emiss_calc
+    g = golden(name)
+    n_ab, n_abc = (int(x) for x in g["n_int"])
+    la_h, la_d = FakeNumpyLinalg(), FakeTorchLinalg()
+    a_h, _, pi_h, _, _ = trans_emiss_calc(*g["args"], n_ab, n_abc, la=la_h)
+    a_d, _, pi_d, _, _ = trans_emiss_calc(*g["args"], n_ab, n_abc, la=la_d)
+    assert la_d.stats["vanloan"] > la_h.stats["vanloan"] > 0  # + the propagator jobs
+    assert np.allclose(a_d, a_h, rtol=1e-12, atol=0) and np.allclose(pi_d, pi_h, rtol=1e-12)
