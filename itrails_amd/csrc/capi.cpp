@@ -680,6 +680,14 @@ int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
     Scope sc("viterbi", st);
     HIP_TRY(itr::launch_vit_hybrid(vh, (int)grid, a, (int)nurg, p->d_cubusy, st));
   } else {
+#ifdef ITR_EXPERIMENT
+    // blocks longer than frac x the longest decode alone on their CU
+    if (getenv("ITR_VIT_EXCL_FRAC")) {
+      a.cu_busy = p->d_cubusy;
+      a.excl_len = std::max<int64_t>(1, (int64_t)(atof(getenv("ITR_VIT_EXCL_FRAC")) *
+                                                  (double)p->sorted_len[0]));
+    }
+#endif
     if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
   }
   itr::TraceArgs ta{};

@@ -35,6 +35,8 @@ struct SweepArgs {
   const int64_t* tile_off;      // [nblocks+1] first tile record of every block (MODE_VIT)
   uint8_t* last_state;          // [nblocks] argmax of the last column (MODE_VIT)
   int prio_len;                 // blocks at least this long run at raised wave priority
+  int* cu_busy;                 // MODE_VIT, optional: [4096] per-CU counts of exclusive blocks
+  int excl_len;                 //   blocks at least this long run alone on their CU
   const int32_t* tasks;         // MODE_FWD_LL: [nblocks x 3] {block, split, slot}, see capi.cpp
   double* svec;                 // MODE_FWD_LL: [nsplit x 2 x XR] vectors of split blocks
   int* sK;                      // MODE_FWD_LL: [nsplit x 2] their power-of-two exponents

@@ -44,16 +44,6 @@ struct VLds {
   static constexpr size_t bytes = (size_t)3 * GM * XB * 8;
 };
 
-// Key of the CU this wave runs on (XCC, shader engine, shader array, CU): the bulk
-// workgroups leave a CU on which a long block is being decoded (cu_busy[key] > 0), so the
-// long block steps alone.  Placement information for speed only, never for correctness.
-__device__ __forceinline__ int cu_key() {
-  const unsigned hw = __builtin_amdgcn_s_getreg(0xF804);   // HW_REG_HW_ID
-  const unsigned xcc = __builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
-  return ((((int)(xcc & 7) * 8 + (int)((hw >> 13) & 7)) * 2 + (int)((hw >> 12) & 1)) * 16 +
-          (int)((hw >> 8) & 0xF));
-}
-
 // One bulk task: blocks grp[0 .. G) (-1: none) stepped in lock-step, QL lanes per (block,
 // target), each taking the max-plus chain over IQ sources; G = (64 W) / (QL n).
 template <int W, int QL, int IQ>

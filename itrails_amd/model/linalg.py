@@ -77,30 +77,42 @@ class DeviceLinalg:
 
     def deepest_t(self, Q: np.ndarray, masks: Dict[Omega, np.ndarray],
                   paths: Sequence[Tuple[Omega, ...]]):
-        """(n_paths, n, n) device tensor: (-C^-1)[:n, -n:] @ (diag(m p[-2]) Q diag(m p[-1]))
-        for each omega path (deepest_ti.py:215-256); the last n columns of C^-1 come from one
-        batched solve against the last n columns of the identity, per path length."""
+        """(n_paths, n, n) device tensor of the deepest-interval integrals (deepest_ti.py:
+        215-256): (-C^-1)[:n, -n:] @ A_{L-1} for the block upper bidiagonal C of path p
+        (diagonal blocks Q, super-diagonal A_i = diag(m p[i-1]) Q diag(m p[i])).  The top-right
+        block of the inverse of such a matrix is (-1)^(L-2) Q^-1 A_1 Q^-1 ... A_{L-2} Q^-1, so
+        the integral is (-1)^(L-1) G_1 G_2 ... G_{L-1} with G_i = Q^-1 A_i: one LU inverse of
+        Q, one batched GEMM for every distinct omega pair, then the chain products per path
+        length (MFMA GEMMs, dense.hip) — instead of one LU of order (L-1) n per path."""
         from ..dense import gemm_batched, solve_batched
         torch = self.torch
         n = Q.shape[0]
         out = torch.empty((len(paths), n, n), dtype=torch.float64, device=self.dev)
+        if not len(paths):
+            return out
+        dQ = torch.from_numpy(np.ascontiguousarray(Q)).to(self.dev)
+        eye = torch.eye(n, dtype=torch.float64, device=self.dev)
+        Qinv = solve_batched(dQ[None].clone(), eye[None].clone())[0]
+        pair_id: Dict = {}
+        for p in paths:
+            for i in range(1, len(p)):
+                pair_id.setdefault((p[i - 1], p[i]), len(pair_id))
+        pl = list(pair_id)
+        ma = torch.from_numpy(np.stack([masks[a] for a, _ in pl]).astype(np.float64)).to(self.dev)
+        mb = torch.from_numpy(np.stack([masks[b] for _, b in pl]).astype(np.float64)).to(self.dev)
+        A = (ma[:, :, None] * dQ[None] * mb[:, None, :]).contiguous()
+        G = gemm_batched(Qinv.expand(len(pl), n, n).contiguous(), A)
         by_len: Dict[int, List[int]] = {}
         for i, p in enumerate(paths):
             by_len.setdefault(len(p), []).append(i)
-        dQ = torch.from_numpy(Q).to(self.dev)
         for L, idx in sorted(by_len.items()):
-            steps = L - 1
-            sub = [paths[i] for i in idx]
-            C = self._block_matrices(Q, masks, sub, steps, None, steps)
-            G = len(sub)
-            R = torch.zeros((G, n * steps, n), dtype=torch.float64, device=self.dev)
-            R[:, (steps - 1) * n:, :] = torch.eye(n, dtype=torch.float64, device=self.dev)
-            X = solve_batched(C, R)[:, :n, :]
-            ma = torch.from_numpy(np.stack([masks[p[-2]] for p in sub]).astype(np.float64)).to(self.dev)
-            mb = torch.from_numpy(np.stack([masks[p[-1]] for p in sub]).astype(np.float64)).to(self.dev)
-            A = (ma[:, :, None] * dQ[None] * mb[:, None, :]).contiguous()
-            out[torch.as_tensor(idx, device=self.dev)] = gemm_batched(X.contiguous(), A,
-                                                                      alpha=-1.0)
+            gi = np.asarray([[pair_id[(paths[i][k - 1], paths[i][k])] for k in range(1, L)]
+                             for i in idx], dtype=np.int64)
+            R = G[torch.from_numpy(gi[:, 0]).to(self.dev)]
+            for k in range(1, L - 1):
+                R = gemm_batched(R.contiguous(),
+                                 G[torch.from_numpy(gi[:, k]).to(self.dev)].contiguous())
+            out[torch.as_tensor(idx, device=self.dev)] = R if (L - 1) % 2 == 0 else -R
         self.stats["deepest"] += len(paths)
         return out
 
