@@ -93,14 +93,20 @@ def load_model(n_int: int):
 WORKLOADS = {"chr10": 10_000_000, "chr100": 100_000_000}
 
 
-def make_workload(kind, a, b, pi, rank, world, mean_block, mbp=None):
-    """-> dict(obs, off, lo, hi, nblocks, cols_total, cols_local, lengths, scaling)."""
+def make_workload(kind, a, b, pi, rank, world, mean_block, mbp=None, block_len=0):
+    """-> dict(obs, off, lo, hi, nblocks, cols_total, cols_local, lengths, scaling).
+    block_len > 0: every block that long (the long-block variant), else geometric lengths."""
     from itrails_amd.distributed import shard_ranges
     from itrails_amd.synth import block_lengths, sample_alignment, sample_alignment_range
 
     cols = int(mbp * 1e6) if mbp else WORKLOADS[kind]
     rng = np.random.default_rng(12345)
-    lengths = block_lengths(rng, cols, mean_block)
+    if block_len > 0:
+        lengths = np.full(cols // block_len, block_len, dtype=np.int64)
+        if cols % block_len:
+            lengths = np.append(lengths, cols % block_len)
+    else:
+        lengths = block_lengths(rng, cols, mean_block)
     if kind == "chr100":
         lo, hi = shard_ranges(lengths, world)[rank]
         obs, off = sample_alignment_range(a, b, pi, lengths, lo, hi, seed=777)
@@ -259,6 +265,9 @@ def main():
     ap.add_argument("--model", choices=["itrails", "introgression"], default="itrails")
     ap.add_argument("--mbp", type=float, default=None, help="override the workload size")
     ap.add_argument("--mean-block", type=float, default=2000.0)
+    ap.add_argument("--block-len", type=int, default=0,
+                    help="fixed block length (long-block variant, e.g. 100000: 10 Mbp = 100 "
+                         "blocks); 0 = geometric lengths of mean --mean-block")
     ap.add_argument("--verify", type=int, default=1,
                     help="1: check every block against the CPU restatement (log-likelihood "
                          "relative error, Viterbi equality); its timing is the CPU baseline")
@@ -308,7 +317,7 @@ def main():
     n = a.shape[0]
     kind = args.workload if args.workload != "auto" else ("chr10" if world == 1 else "chr100")
     t0 = time.time()
-    W = make_workload(kind, a, b, pi, rank, world, args.mean_block, args.mbp)
+    W = make_workload(kind, a, b, pi, rank, world, args.mean_block, args.mbp, args.block_len)
     gen_s = time.time() - t0
     obs, off, lo = W["obs"], W["off"], W["lo"]
 
@@ -349,7 +358,8 @@ def main():
         _, (a1, b1, p1, _, _) = build(x, names, frozenset(["t_1"]),
                                       {"n_int_AB": args.n_int, "n_int_ABC": args.n_int})
         m1 = hmm.Model(a1, b1, p1)
-        build_ms.append((time.perf_counter() - tb) * 1e3)
+        if timing:
+            build_ms.append((time.perf_counter() - tb) * 1e3)
         hmm.forward_loglik_device(m1, plan, d_obs, out=d_ll)
         if timing:
             fwd_ms.append(hmm.last_kernel_ms("forward"))
@@ -508,8 +518,10 @@ def main():
             "scaling": W["scaling"],
             "vs_baseline": None,
             "dtype": "f64",
-            "data": f"synthetic: columns sampled from the {model_name}, geometric blocks mean "
-                    f"{args.mean_block:g} columns, 1% gaps + 0.5% N",
+            "data": f"synthetic: columns sampled from the {model_name}, " +
+                    (f"blocks of {args.block_len} columns" if args.block_len > 0 else
+                     f"geometric blocks mean {args.mean_block:g} columns") +
+                    ", 1% gaps + 0.5% N",
             "config": {"workload": f"{kind}: {cols_total / 1e6:g} Mbp " +
                                    ("alignment sharded over the ranks" if W["scaling"] == "strong"
                                     else "per GPU") + f", {args.n_int}+{args.n_int} intervals, " +
