@@ -106,7 +106,6 @@ struct VitHybridGeometry {
   int G;        // blocks per lock-step group
   size_t lds;   // dynamic LDS bytes
   int per_cu;   // resident workgroups per CU
-  int exit_busy;  // bulk workgroups on a CU decoding a long block: 0 wait, 1 exit, -1 ignore
 };
 VitHybridGeometry vit_hybrid_geometry(int n);
 // v.order[0, nurg) as VALU tasks, then groups of v.order[nurg, v.nblocks); v.queue[0..1]
