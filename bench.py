@@ -275,6 +275,9 @@ def main():
                     help="columns of the 1-core CPU-baseline sample (0 = skip)")
     ap.add_argument("--host-path", type=int, default=1,
                     help="1: also time the drop-in wrappers on host NumPy buffers (N = 1)")
+    ap.add_argument("--split-build", type=int, default=1, choices=[0, 1],
+                    help="optimize mode, N > 1: divide each rebuild's Van Loan work over the "
+                         "ranks (one RCCL all-gather) instead of rebuilding on every rank")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the exchange with several ranks on one GPU)")
@@ -354,9 +357,11 @@ def main():
         names = list(base)
         x = [base[k] * (1.0 + 1e-3 * ((eval_no[0] + i) % 5 - 2)) for i, k in enumerate(names)]
         tb = time.perf_counter()
+        from itrails_amd.model.linalg import split_build
         build = model_for_introgression if intro else model_for
-        _, (a1, b1, p1, _, _) = build(x, names, frozenset(["t_1"]),
-                                      {"n_int_AB": args.n_int, "n_int_ABC": args.n_int})
+        with split_build(world > 1 and args.backend == "nccl" and args.split_build == 1):
+            _, (a1, b1, p1, _, _) = build(x, names, frozenset(["t_1"]),
+                                          {"n_int_AB": args.n_int, "n_int_ABC": args.n_int})
         m1 = hmm.Model(a1, b1, p1)
         if timing:
             build_ms.append((time.perf_counter() - tb) * 1e3)

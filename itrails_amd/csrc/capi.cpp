@@ -122,6 +122,12 @@ struct itr_plan {
   int64_t* d_off = nullptr;
   int64_t* d_tile_off = nullptr;  // [nblocks+1] first tile record of every block
   int* d_cubusy = nullptr;        // [4096] per-CU long-block counts (Viterbi hybrid)
+  // posterior split (launch_post_split): the first npsplit blocks of the order get their
+  // backward sweep concurrently with the forward one; beta rows at d_boff[block]
+  int64_t npsplit = 0, beta_rows = 0;
+  int64_t* d_boff = nullptr;
+  double* d_beta = nullptr;
+  size_t beta_cap = 0;
   int32_t* d_order = nullptr;
   int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
@@ -194,6 +200,11 @@ int reserve(itr_plan_t p, int n, bool vit, bool post) {
     const int stride = g.cfg >= 0 ? std::max(xa, g.xr) : xa;
     need_rows = std::max(need_rows, (size_t)p->total * stride);
   }
+  if (post && p->beta_rows > 0 && (size_t)p->beta_rows * xa > p->beta_cap) {
+    dev_free(p->d_beta);
+    if (int e = dev_alloc(&p->d_beta, (size_t)p->beta_rows * xa)) return e;
+    p->beta_cap = (size_t)p->beta_rows * xa;
+  }
   if (need_rows > p->alpha_cap) {
     dev_free(p->d_alpha);
     if (int e = dev_alloc(&p->d_alpha, need_rows)) return e;
@@ -227,6 +238,7 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname) {
   int64_t grid = (int64_t)g.per_cu * cu_count();
   if (grid > a.nblocks) grid = a.nblocks;
   if (grid <= 0) return 0;
+  if (grid <= cu_count()) g.lds = std::max(g.lds, itr::kExclusiveLds);  // one per CU
   HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
 #ifdef ITR_DIAG
   if (getenv("ITR_VERBOSE"))
@@ -285,6 +297,8 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
 #endif
   int64_t grid = std::min<int64_t>((int64_t)per_cu * cu_count(), work);
   if (grid <= 0) return 0;
+  itr::MfmaGeometry gx = g;
+  if (grid <= cu_count()) gx.lds_min = itr::kExclusiveLds;  // one workgroup per CU
   HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
 #ifdef ITR_DIAG
   if (getenv("ITR_VERBOSE"))
@@ -293,7 +307,7 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
             (long long)a.ngroups);
 #endif
   Scope sc(tname, st);
-  HIP_TRY(itr::launch_hybrid_sweep(mode, g, (int)grid, a, v, st));
+  HIP_TRY(itr::launch_hybrid_sweep(mode, gx, (int)grid, a, v, st));
   return 0;
 }
 
@@ -430,6 +444,22 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
       split_blk.push_back(b);
     }
   }
+  // posterior split set (blocks at least a quarter as long as the longest, >= 512 columns;
+  // ITR_POST_SPLIT_FRAC read once here, 0 disables): a prefix of the order
+  std::vector<int64_t> boff(nblocks, -1);
+  {
+    const char* pf = getenv("ITR_POST_SPLIT_FRAC");
+    const double pfrac = pf ? atof(pf) : 0.25;
+    int64_t rows = 0, k = 0;
+    for (; k < nblocks; ++k) {
+      const int64_t T = h_off[order[k] + 1] - h_off[order[k]];
+      if (!(pfrac > 0 && T >= 512 && (double)T >= pfrac * (double)tmax)) break;
+      boff[order[k]] = rows;
+      rows += T;
+    }
+    p->npsplit = k;
+    p->beta_rows = rows;
+  }
   auto make_tasks = [&](int64_t count) {
     std::vector<int32_t> tasks;
     std::vector<int64_t> tlen;
@@ -546,6 +576,7 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   if (!e) e = dev_alloc(&p->d_sK, nslots * 2);
   if (!e) e = dev_alloc(&p->d_off, nblocks + 1);
   if (!e) e = dev_alloc(&p->d_tile_off, nblocks + 1);
+  if (!e) e = dev_alloc(&p->d_boff, nblocks);
   if (!e) e = dev_alloc(&p->d_cubusy, 4096);
   if (!e && hipMemset(p->d_cubusy, 0, 4096 * sizeof(int)) != hipSuccess)
     e = fail(ITR_EHIP, "plan workspace init failed");
@@ -560,6 +591,7 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   };
   up(p->d_off, h_off.data(), (nblocks + 1) * sizeof(int64_t));
   up(p->d_tile_off, tile_off.data(), (nblocks + 1) * sizeof(int64_t));
+  up(p->d_boff, boff.data(), nblocks * sizeof(int64_t));
   up(p->d_order, order.data(), nblocks * sizeof(int32_t));
   up(p->d_tasks, tasks.data(), tasks.size() * sizeof(int32_t));
   up(p->d_utasks, utasks.data(), utasks.size() * sizeof(int32_t));
@@ -580,6 +612,8 @@ int itr_plan_destroy(itr_plan_t p) {
   dev_free(p->d_off);
   dev_free(p->d_tile_off);
   dev_free(p->d_cubusy);
+  dev_free(p->d_boff);
+  dev_free(p->d_beta);
   dev_free(p->d_order);
   dev_free(p->d_queue);
   dev_free(p->d_sink);
@@ -733,6 +767,39 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
     if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, st, "posterior_fwd")) return e;
     a.post = post;
     return run_hybrid(itr::MODE_BWD, m, p, a, gb, st, "posterior_bwd");
+  }
+  const int nl = (int)p->npsplit;
+  // only where the blocks are few (latency-bound: 10 Mbp in 100 blocks of 100 kbp, 96.9 ->
+  // 60 ms); with thousands of blocks the sweeps are throughput-bound and the extra beta
+  // rows cost more than the shorter tail (chr10: 20.7 vs 23.4 ms)
+  if (nl > 0 && m->n <= 128 && p->nblocks <= 2 * (int64_t)cu_count()) {
+    // the longest blocks: backward sweep (beta rows) concurrently with every block's forward
+    // sweep; then the short blocks' backward+posterior sweep and the long blocks' combine
+    itr::SweepGeometry g = itr::sweep_geometry(m->n, itr::MODE_BWD);
+    if (g.iq < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", m->n);
+    a.xp = g.xp;
+    itr::SweepArgs b = a;
+    b.beta = p->d_beta;
+    b.beta_off = p->d_boff;
+    const int64_t grid = std::min<int64_t>((int64_t)g.per_cu * cu_count(), p->nblocks + nl);
+    if (grid <= cu_count()) g.lds = std::max(g.lds, itr::kExclusiveLds);
+    HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
+    {
+      Scope sc("posterior_fwd", st);
+      HIP_TRY(itr::launch_post_split(g, (int)grid, a, b, nl, st));
+    }
+    itr::SweepArgs c = a;
+    c.post = post;
+    Scope sc("posterior_bwd", st);  // the short blocks' sweep + the long blocks' combine
+    if (p->nblocks > nl) {
+      c.order = p->d_order + nl;
+      c.nblocks = p->nblocks - nl;
+      if (int e = run_sweep(itr::MODE_BWD, c, st, "posterior_bwd_short")) return e;
+    }
+    HIP_TRY(itr::launch_post_combine(m->n, itr::sweep_row_stride(m->n, itr::MODE_BWD), nl,
+                                     p->sorted_len[0], p->d_order, p->d_off, p->d_alpha,
+                                     p->d_beta, p->d_boff, post, st));
+    return 0;
   }
   if (int e = run_sweep(itr::MODE_FWD_STORE, a, st, "posterior_fwd")) return e;
   a.post = post;

@@ -332,6 +332,92 @@ hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepA
   return dispatch_mode(mode, g.iq, true, &a, grid, g.lds, st, &occ);
 }
 
+// ---------------------------------------------------------------------------------------
+// Posterior of long blocks, forward and backward concurrently.  The posterior needs
+// alpha_t and beta_t at every column; alpha depends only on the block's start and beta only
+// on its end, so for the longest blocks the backward sweep need not wait for the forward
+// one: one persistent launch takes the long blocks' backward sweeps (storing beta rows) and
+// every block's forward sweep (storing alpha rows) from one queue, long backward tasks first;
+// the short blocks' backward+posterior sweep follows as usual and post_combine_kernel forms
+// the long blocks' posteriors from the two stored rows.  The critical path drops from 2 T
+// to T + (the longest short block) for the longest block's T.
+template <int QL, int WV, int RJN, int IQ>
+__global__ void __launch_bounds__(64 * WV, (Occ<QL, WV, RJN, IQ, MODE_BWD>::value))
+    post_split_kernel(SweepArgs f, SweepArgs b, int nlong) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int qslot;
+  for (;;) {
+    if (threadIdx.x == 0) qslot = atomicAdd(f.queue, 1);
+    lds_barrier();
+    const int bi = uni(qslot);
+    lds_barrier();
+    if (bi < nlong) {
+      sweep_task<QL, WV, RJN, IQ, MODE_BWD>(b, smem, bi);
+    } else if (bi - nlong < f.nblocks) {
+      sweep_task<QL, WV, RJN, IQ, MODE_FWD_STORE>(f, smem, bi - nlong);
+    } else {
+      break;
+    }
+  }
+}
+
+hipError_t launch_post_split(const SweepGeometry& g, int grid, const SweepArgs& f,
+                             const SweepArgs& b, int nlong, hipStream_t st) {
+#define ITR_PS(C, QL, WV, RJN, IQ)                                                           \
+  case C:                                                                                    \
+    hipLaunchKernelGGL((post_split_kernel<QL, WV, RJN, IQ>), dim3(grid), dim3(64 * WV), g.lds, \
+                       st, f, b, nlong);                                                     \
+    return hipGetLastError();
+  switch (g.iq) {  // the configurations pick_cfg gives the probability sweeps
+    ITR_PS(0, 8, 4, 1, 4)
+    ITR_PS(1, 8, 4, 2, 8)
+    ITR_PS(2, 8, 4, 3, 9)
+    ITR_PS(3, 8, 4, 3, 12)
+    ITR_PS(4, 8, 4, 4, 16)
+    ITR_PS(5, 8, 4, 5, 17)
+    ITR_PS(6, 8, 4, 6, 24)
+    ITR_PS(20, 8, 3, 3, 9)
+    ITR_PS(21, 8, 6, 3, 17)
+  }
+#undef ITR_PS
+  return hipErrorInvalidValue;
+}
+
+// posteriors of the split blocks' columns: alpha_t * beta_t / sum_j alpha_t[j] beta_t[j]
+// (the backward sweep's own expression, optimizer.py:228-238); one wave per column
+__global__ void __launch_bounds__(256) post_combine_kernel(int n, int xr, const int32_t* order,
+                                                           const int64_t* off,
+                                                           const double* alpha,
+                                                           const double* beta,
+                                                           const int64_t* beta_off,
+                                                           double* post) {
+  const int blk = order[blockIdx.y];
+  const int64_t c0 = off[blk];
+  const int64_t T = off[blk + 1] - c0;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const int l = threadIdx.x & 63;
+  const double* a = alpha + (c0 + t) * xr;
+  const double* b = beta + (beta_off[blk] + t) * xr;
+  const double q0 = l < n ? a[l] * b[l] : 0.0;
+  const double q1 = l + 64 < n ? a[l + 64] * b[l + 64] : 0.0;
+  const double S = wave_sum(q0 + q1);
+  const double rS = 1.0 / S;
+  double* dst = post + (c0 + t) * n;
+  if (l < n) dst[l] = q0 * rS;
+  if (l + 64 < n) dst[l + 64] = q1 * rS;
+}
+
+hipError_t launch_post_combine(int n, int xr, int nlong, int64_t tmax, const int32_t* order,
+                               const int64_t* off, const double* alpha, const double* beta,
+                               const int64_t* beta_off, double* post, hipStream_t st) {
+  if (nlong <= 0 || tmax <= 0) return hipSuccess;
+  if (n > 128) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(post_combine_kernel, dim3((unsigned)((tmax + 3) / 4), (unsigned)nlong),
+                     dim3(256), 0, st, n, xr, order, off, alpha, beta, beta_off, post);
+  return hipGetLastError();
+}
+
 int sweep_row_stride(int n, int mode) {  // padded target states: row stride of bp / alpha
   const int c = pick_cfg(n, mode);
   return c < 0 ? -1 : cfg_xr(c);

@@ -442,8 +442,9 @@ size_t lds_h() {
   return std::max(MLds<NT, NK, GB>::bytes, V::lds_bytes);
 }
 template <int NT, int NK, int GB, int MODE, int VIQ>
-hipError_t launch_h(const MfmaArgs& a, const SweepArgs& v, int grid, hipStream_t st) {
-  const size_t lds = lds_h<NT, NK, GB, MODE, VIQ>();
+hipError_t launch_h(const MfmaArgs& a, const SweepArgs& v, int grid, size_t lds_min,
+                    hipStream_t st) {
+  const size_t lds = std::max(lds_h<NT, NK, GB, MODE, VIQ>(), lds_min);
   hipLaunchKernelGGL((hybrid_sweep_kernel<NT, NK, GB, MODE, 2, VIQ>), dim3(grid), dim3(64 * NT),
                      lds, st, a, v);
   return hipGetLastError();
@@ -460,10 +461,10 @@ int occ_h() {
 
 template <int MODE>
 hipError_t dispatch_m(int c, bool launch, const MfmaArgs* a, const SweepArgs* v, int grid,
-                      hipStream_t st, int* occ) {
+                      size_t lds_min, hipStream_t st, int* occ) {
 #define ITR_MCFG(C, NT, NK, GB, VIQ)                                        \
   case C:                                                                   \
-    if (launch) return launch_h<NT, NK, GB, MODE, VIQ>(*a, *v, grid, st);   \
+    if (launch) return launch_h<NT, NK, GB, MODE, VIQ>(*a, *v, grid, lds_min, st); \
     *occ = occ_h<NT, NK, GB, MODE, VIQ>();                                  \
     return hipSuccess;
   switch (c) {
@@ -481,11 +482,12 @@ hipError_t dispatch_m(int c, bool launch, const MfmaArgs* a, const SweepArgs* v,
 }
 
 hipError_t dispatch_mode_m(int mode, int c, bool launch, const MfmaArgs* a, const SweepArgs* v,
-                           int grid, hipStream_t st, int* occ) {
+                           int grid, size_t lds_min, hipStream_t st, int* occ) {
   switch (mode) {
-    case MODE_FWD_LL: return dispatch_m<MODE_FWD_LL>(c, launch, a, v, grid, st, occ);
-    case MODE_FWD_STORE: return dispatch_m<MODE_FWD_STORE>(c, launch, a, v, grid, st, occ);
-    case MODE_BWD: return dispatch_m<MODE_BWD>(c, launch, a, v, grid, st, occ);
+    case MODE_FWD_LL: return dispatch_m<MODE_FWD_LL>(c, launch, a, v, grid, lds_min, st, occ);
+    case MODE_FWD_STORE:
+      return dispatch_m<MODE_FWD_STORE>(c, launch, a, v, grid, lds_min, st, occ);
+    case MODE_BWD: return dispatch_m<MODE_BWD>(c, launch, a, v, grid, lds_min, st, occ);
   }
   return hipErrorInvalidValue;
 }
@@ -521,7 +523,7 @@ MfmaGeometry mfma_geometry(int n, int mode) {
   if (getenv("ITR_POST_URGENT_FRAC")) g.pfrac = atof(getenv("ITR_POST_URGENT_FRAC"));
 #endif
   int occ = 1;
-  (void)dispatch_mode_m(mode, g.cfg, false, nullptr, nullptr, 0, nullptr, &occ);
+  (void)dispatch_mode_m(mode, g.cfg, false, nullptr, nullptr, 0, 0, nullptr, &occ);
   g.per_cu = occ;
   return g;
 }
@@ -529,7 +531,7 @@ MfmaGeometry mfma_geometry(int n, int mode) {
 hipError_t launch_hybrid_sweep(int mode, const MfmaGeometry& g, int grid, const MfmaArgs& a,
                                const SweepArgs& v, hipStream_t st) {
   int occ = 0;
-  return dispatch_mode_m(mode, g.cfg, true, &a, &v, grid, st, &occ);
+  return dispatch_mode_m(mode, g.cfg, true, &a, &v, grid, g.lds_min, st, &occ);
 }
 
 }  // namespace itr

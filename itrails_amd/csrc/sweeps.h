@@ -35,6 +35,9 @@ struct SweepArgs {
   const int64_t* tile_off;      // [nblocks+1] first tile record of every block (MODE_VIT)
   uint8_t* last_state;          // [nblocks] argmax of the last column (MODE_VIT)
   int prio_len;                 // blocks at least this long run at raised wave priority
+  double* beta;                 // MODE_BWD, optional: store the backward rows beta_t here
+                                //   (row beta_off[block] + t, stride XR) instead of posteriors
+  const int64_t* beta_off;      //   [nblocks] first beta row of every split block
   int* cu_busy;                 // MODE_VIT, optional: [4096] per-CU counts of exclusive blocks
   int excl_len;                 //   blocks at least this long run alone on their CU
   const int32_t* tasks;         // MODE_FWD_LL: [nblocks x 3] {block, split, slot}, see capi.cpp
@@ -56,6 +59,16 @@ SweepGeometry sweep_geometry(int n, int mode);
 // row stride (padded states) of the back-pointer rows (MODE_VIT) / forward rows (FWD_STORE,
 // BWD: both use the same configuration)
 int sweep_row_stride(int n, int mode);
+
+// Posterior of long blocks with concurrent forward and backward sweeps (hmm_sweeps.hip):
+// one persistent launch running f (MODE_FWD_STORE over f.nblocks blocks of f.order) and, for
+// the first nlong blocks of b.order, the backward sweep storing its rows into b.beta; then
+// post_combine forms alpha_t beta_t / sum_j alpha_t beta_t for those blocks' columns.
+hipError_t launch_post_split(const SweepGeometry& g, int grid, const SweepArgs& f,
+                             const SweepArgs& b, int nlong, hipStream_t st);
+hipError_t launch_post_combine(int n, int xr, int nlong, int64_t tmax, const int32_t* order,
+                               const int64_t* off, const double* alpha, const double* beta,
+                               const int64_t* beta_off, double* post, hipStream_t st);
 hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepArgs& a,
                         hipStream_t st);
 
@@ -89,7 +102,13 @@ struct MfmaGeometry {
   int gb;       // groups per workgroup
   int per_cu;   // resident workgroups per CU (occupancy API)
   double pfrac; // posterior sweeps: blocks longer than pfrac x the longest are VALU tasks
+  size_t lds_min;  // launch with at least this much LDS (kExclusiveLds: one workgroup per CU)
 };
+
+// Dynamic LDS that leaves room for one workgroup per CU (160 KiB LDS per CU): requested when
+// a launch has no more tasks than CUs, so the dispatcher cannot stack two of them on one CU
+// (two co-resident sweeps step at ~1.6x the lone step time).
+constexpr size_t kExclusiveLds = 81 * 1024;
 MfmaGeometry mfma_geometry(int n, int mode);
 // one launch: the VALU tasks of `v` (v.tasks / v.order, v.nblocks of them: the longest
 // blocks, on the VALU configuration {8 lanes, g.block / 64 waves, 2 targets per lane}, whose

@@ -350,7 +350,10 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
       est.issue(p.emit, n, n, tid, 0, sym_row);
       est.commit(EST, tid);
       est.issue(p.emit, n, n, tid, TE, sym_row);
-      if constexpr (MODE == MODE_BWD) {
+      // MODE_BWD with p.beta (the posterior's concurrent split) stores beta rows and needs no
+      // forward rows
+      const bool need_alpha = MODE == MODE_BWD && !p.beta;
+      if (need_alpha) {
         ast.issue(p.alpha, XR, XR, tid, 0, fwd_row);
         ast.commit(AST, tid);
         ast.issue(p.alpha, XR, XR, tid, TE, fwd_row);
@@ -360,14 +363,14 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
         if (s >= TE && (s & (TE - 1)) == 0) {
           const int slot = (s / TE) & 1;
           est.commit(EST + slot * TE * XR, tid);
-          if constexpr (MODE == MODE_BWD) ast.commit(AST + slot * TE * XR, tid);
+          if (need_alpha) ast.commit(AST + slot * TE * XR, tid);
         }
       };
       // ... and request the one after it behind the barrier
       auto stage_issue = [&](int s) {
         if (s >= TE && (s & (TE - 1)) == 0) {
           est.issue(p.emit, n, n, tid, s + TE, sym_row);
-          if constexpr (MODE == MODE_BWD) ast.issue(p.alpha, XR, XR, tid, s + TE, fwd_row);
+          if (need_alpha) ast.issue(p.alpha, XR, XR, tid, s + TE, fwd_row);
         }
       };
       auto staged = [&](const double* base, int s, int j) {
@@ -533,13 +536,18 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
               double qv[RJN], v[RJN], ps = 0.0;
 #pragma unroll
               for (int r = 0; r < RJN; ++r) {
-                qv[r] = staged(AST, s, jr[r]) * bt[r];  // padded states: 0 * 0
-                ps += qv[r];
                 v[r] = bt[r] * staged(EST, s, jr[r]);
                 Xb[jx[r]] = v[r];
               }
-              ps = row_sum<QL>(ps);  // the row's target-state groups
-              if (row_leader) RED[buf * 64 + row16] = ps;
+              if (need_alpha) {
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) {
+                  qv[r] = staged(AST, s, jr[r]) * bt[r];  // padded states: 0 * 0
+                  ps += qv[r];
+                }
+                ps = row_sum<QL>(ps);  // the row's target-state groups
+                if (row_leader) RED[buf * 64 + row16] = ps;
+              }
               const bool rescale = (sub & 7) == 0;
               if (rescale) {
                 double mx = v[0];
@@ -552,14 +560,22 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
               if (sub == TE - 1) stage_commit(s + 1);
               lds_barrier();
               if (sub == TE - 1) stage_issue(s + 1);
-              double S = 0.0;
+              if (p.beta) {
+                // concurrent split (launch_post_split): this block's forward rows are being
+                // written by another workgroup, so store beta_t for post_combine instead
+                const int64_t brow = (p.beta_off[blk] + t) * XR;
 #pragma unroll
-              for (int u = 0; u < NROW; ++u) S += RED[buf * 64 + u];
-              const double rS = 1.0 / S;
+                for (int r = 0; r < RJN; ++r) p.beta[brow + jr[r]] = bt[r];
+              } else {
+                double S = 0.0;
 #pragma unroll
-              for (int r = 0; r < RJN; ++r) {
-                double* dst = jv[r] ? p.post + (c0 + t) * n + jr[r] : sink;
-                *dst = qv[r] * rS;
+                for (int u = 0; u < NROW; ++u) S += RED[buf * 64 + u];
+                const double rS = 1.0 / S;
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) {
+                  double* dst = jv[r] ? p.post + (c0 + t) * n + jr[r] : sink;
+                  *dst = qv[r] * rS;
+                }
               }
               double sc = 1.0;
               if (rescale) {

@@ -516,6 +516,62 @@ def _group_matrices(S, steps, ng, n):
     return M
 
 
+def _interval_mats_split(plan, tab, Q, t, la):
+    """(E_i, M_i) of every interval with the Van Loan work divided over the ranks of
+    la.group: rank r evaluates intervals i = r, r + world, ... (their Van Loan paths and
+    propagators in one itr_vanloan_paths call) and their path-group sums; one all-gather of
+    [E_i, M_i] slots (zero-padded to the largest group count) shares them."""
+    import torch
+    import torch.distributed as dist
+    rank, world = la.rank, la.world
+    n = Q.shape[0]
+    ivs = tab["ivs"]
+    I = len(ivs)
+    key = ("split", rank, world)
+    if key not in tab:
+        mine = [i for i in range(I) if i % world == rank]
+        job, off0, pm, loc = [], [0], [], []
+        for k, i in enumerate(mine):
+            d = ivs[i]
+            a, b = d.vl0, d.vl1
+            lo = len(job)
+            for p in range(a, b):
+                job.append(2 * k)
+                off0.append(off0[-1] + int(tab["off"][p + 1] - tab["off"][p]))
+                pm.extend(tab["pm"][tab["off"][p]:tab["off"][p + 1]].tolist())
+            e = len(job)
+            job.append(2 * k + 1)
+            off0.append(off0[-1] + 1)
+            pm.append(0)
+            loc.append((lo, e))
+        tab[key] = (mine, np.asarray(job, dtype=np.int32), np.asarray(off0, dtype=np.int64),
+                    np.asarray(pm, dtype=np.int32), loc)
+    mine, job, off0, pm, loc = tab[key]
+    slots = (I + world - 1) // world
+    gmax = max(d.ng for d in ivs)
+    buf = torch.zeros((slots, 1 + gmax, n, n), dtype=torch.float64, device=la.dev)
+    if mine:
+        tl = np.asarray([t[i] if j % 2 == 0 else t[I + i] for i in mine for j in (0, 1)],
+                        dtype=np.float64)
+        S = la.vanloan_batch(Q, tab["mask_u8"], tl, job, off0, pm)
+        for k, i in enumerate(mine):
+            d = ivs[i]
+            lo, e = loc[k]
+            buf[k, 0] = S[e]
+            if d.ng:
+                buf[k, 1:1 + d.ng] = _group_matrices(S[lo:e], d.sum_steps, d.ng, n)
+    if buf.is_cuda and dist.get_backend(la.group) != "nccl":
+        buf = buf.cpu()  # gloo rehearsal of the exchange (tests: ranks sharing one GPU)
+    got = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(got, buf, group=la.group)
+    got = [x.to(la.dev) for x in got]
+    out = []
+    for i, d in enumerate(ivs):
+        g = got[i % world][i // world]
+        out.append((g[0], g[1:1 + d.ng] if d.ng else None))
+    return out
+
+
 def _run_chain_abc_device(plan, Q, times, ss, probs: Dict, la) -> Dict:
     """_run_chain_abc_planned with every number resident on the device: one shared Van Loan
     evaluation for all intervals (their propagators included), the key rows as one
@@ -528,21 +584,26 @@ def _run_chain_abc_device(plan, Q, times, ss, probs: Dict, la) -> Dict:
     dev = la.dev
     I = len(plan.intervals)
     t = np.asarray([times[i] for i in range(I)] * 2, dtype=np.float64)
-    S_all = la.vanloan_batch(Q, tab["mask_u8"], t, tab["job"], tab["off"], tab["pm"])
+    if getattr(la, "world", 1) > 1:
+        EM = _interval_mats_split(plan, tab, Q, t, la)
+    else:
+        S_all = la.vanloan_batch(Q, tab["mask_u8"], t, tab["job"], tab["off"], tab["pm"])
+        EM = [(S_all[d.e_idx],
+               _group_matrices(S_all[d.vl0:d.vl1], d.sum_steps, d.ng, n) if d.ng else None)
+              for d in tab["ivs"]]
     F = tab["F"]
     P = torch.zeros((plan.nrows, n), dtype=torch.float64, device=dev)
     P0 = np.zeros((len(probs), n))
     for i, v in enumerate(probs.values()):
         P0[i] = v[0]
     P[:len(probs)] = torch.from_numpy(P0).to(dev)
-    for d in tab["ivs"]:
+    for d, (E, M) in zip(tab["ivs"], EM):
         Pn = P.clone()
         if d.plain is not None:
             src, oms, ome, dst = d.plain
-            Pn[dst] = ((P[src] * F[oms]) @ S_all[d.e_idx]) * F[ome]
+            Pn[dst] = ((P[src] * F[oms]) @ E) * F[ome]
         if d.rows is not None:
             src, oms, ome, dst, gid, slot = d.rows
-            M = _group_matrices(S_all[d.vl0:d.vl1], d.sum_steps, d.ng, n)
             V = torch.zeros((d.ng, d.rmax, n), dtype=torch.float64, device=dev)
             V[gid, slot] = P[src] * F[oms]
             Pn[dst] = torch.bmm(V, M)[gid, slot] * F[ome]

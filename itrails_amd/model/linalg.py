@@ -9,11 +9,31 @@ assembled on the device and evaluated as one batch by the HIP kernels of dense.h
 """
 from __future__ import annotations
 
+from contextlib import contextmanager
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
 
 Omega = Tuple[int, int]
+
+_SPLIT_GROUP = [None]  # process group of a rank-split model build, see split_build
+
+
+@contextmanager
+def split_build(enabled: bool = True, group=None):
+    """Model builds started inside this context on a torch.distributed job divide their
+    de-duplicated Van Loan work across the ranks of `group` (run_markov_chain_ABC.py:118-195
+    fans the reference's tasks out over processes the same way): interval i of the
+    three-species chain is evaluated by rank i mod world, which also forms its path-group
+    sums; one all-gather gives every rank all intervals' propagators and group matrices.
+    Every rank of the group must build the same model at the same time (the optimizer's
+    objective evaluations do)."""
+    prev = _SPLIT_GROUP[0]
+    _SPLIT_GROUP[0] = ("on", group) if enabled else None
+    try:
+        yield
+    finally:
+        _SPLIT_GROUP[0] = prev
 
 
 class DeviceLinalg:
@@ -26,6 +46,13 @@ class DeviceLinalg:
         self.torch = torch
         self.dev = torch.device("cuda", torch.cuda.current_device())
         self.stats = {"expm": 0, "vanloan": 0, "deepest": 0}
+        self.rank, self.world, self.group = 0, 1, None
+        if _SPLIT_GROUP[0] is not None:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                self.group = _SPLIT_GROUP[0][1]
+                self.rank = dist.get_rank(self.group)
+                self.world = dist.get_world_size(self.group)
 
     def expm(self, mats: Sequence[np.ndarray]) -> List[np.ndarray]:
         from ..dense import expm_batched

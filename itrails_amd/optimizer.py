@@ -90,12 +90,21 @@ def model_for(arg_lst, optimized_params: Sequence[str], case: frozenset, d: Dict
                                 dd["n_int_AB"], dd["n_int_ABC"], "standard", "standard")
 
 
+def _nccl() -> bool:
+    import torch.distributed as dist
+    return dist.is_initialized() and dist.get_backend() == "nccl"
+
+
 def optimization_wrapper(arg_lst, optimized_params, case, d, data: DeviceAlignment,
                          res_name: str, info: Dict) -> float:
     """optimizer.py:396-585: one objective evaluation -> -loglik, with the history row and
     the best-model update the reference writes (rank 0 only when distributed)."""
     output_dir, output_prefix = os.path.split(res_name)
-    _, (a, b, pi, _, _) = model_for(arg_lst, optimized_params, case, d)
+    from .model.linalg import split_build
+    # multi-GPU: the rebuild's Van Loan work is divided over the ranks (every rank
+    # evaluates the same parameters at the same time)
+    with split_build(data.dist and _nccl(), data.group):
+        _, (a, b, pi, _, _) = model_for(arg_lst, optimized_params, case, d)
     loglik = data.loglik(a, b, pi)
     if _is_writer():
         write_list([info["Nfeval"]] + list(np.asarray(arg_lst).tolist()) +

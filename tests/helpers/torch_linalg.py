@@ -23,12 +23,18 @@ def _fake(n, rows, t):
     return rng.random((n, n)) * 1e-2
 
 
+def _fake_q(Qt):
+    """Stand-in for expm(Q t) (a length-1 path or an interval propagator), seeded by the
+    matrix Q t itself so both requests get the same matrix."""
+    return _fake(Qt.shape[0], [np.ascontiguousarray(Qt)], 0.0)
+
+
 class FakeNumpyLinalg(NumpyLinalg):
     def vanloan(self, Q, t, masks, paths):
         self.stats["vanloan"] += len(paths)
         n = Q.shape[0]
-        return [_fake(n, [np.asarray(masks[w], dtype=np.uint8) for w in p] if len(p) > 1
-                      else [], t) for p in paths]
+        return [_fake(n, [np.asarray(masks[w], dtype=np.uint8) for w in p], t) if len(p) > 1
+                else _fake_q(Q * t) for p in paths]
 
     def deepest(self, Q, masks, paths):
         self.stats["deepest"] += len(paths)
@@ -38,24 +44,22 @@ class FakeNumpyLinalg(NumpyLinalg):
 
     def expm(self, mats):  # interval propagators: a length-1 "path"
         self.stats["expm"] += len(mats)
-        return [_fake(m.shape[0], [], float(np.abs(m).sum())) if m.shape[0] > 100
-                else super(FakeNumpyLinalg, self).expm([m])[0] for m in mats]
+        return [_fake_q(m) if m.shape[0] > 100 else super(FakeNumpyLinalg, self).expm([m])[0]
+                for m in mats]
 
 
 class FakeTorchLinalg(FakeNumpyLinalg):
     dev = torch.device("cpu")
+    rank, world, group = 0, 1, None
 
     def vanloan_batch(self, Q, masks_u8, t, path_job, path_off, path_mask):
         n = Q.shape[0]
         out = []
-        I = len(t) // 2
         for p in range(len(path_job)):
             ids = path_mask[path_off[p]:path_off[p + 1]]
             j = int(path_job[p])
-            if j >= I:  # the propagator job of interval j - I: what expm() above returns
-                out.append(_fake(n, [], float(np.abs(Q * t[j]).sum())))
-            else:
-                out.append(_fake(n, [masks_u8[i] for i in ids] if len(ids) > 1 else [], t[j]))
+            out.append(_fake(n, [np.asarray(masks_u8[i], dtype=np.uint8) for i in ids], t[j])
+                       if len(ids) > 1 else _fake_q(Q * t[j]))
         self.stats["vanloan"] += len(path_job)
         return torch.from_numpy(np.stack(out)) if out else torch.zeros((0, n, n),
                                                                        dtype=torch.float64)

@@ -123,3 +123,50 @@ def test_sharded_sampling_independent_of_world_size():
             ref = allobs
         assert np.array_equal(allobs, ref)
     assert len(ref) == 300_000
+
+
+def _split_build_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    os.environ["OMP_NUM_THREADS"] = "1"
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        from helpers.torch_linalg import FakeTorchLinalg
+        from itrails_amd.model import trans_emiss_calc
+        g = golden("model_kat_3_3.npz")
+        la = FakeTorchLinalg()
+        la.rank, la.world = rank, world
+        a, _, pi, _, _ = trans_emiss_calc(*g["args"], 3, 3, la=la)
+        q.put((rank, a, pi, la.stats["vanloan"]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_model_build_gloo_matches_single_rank(world):
+    """The rank-split model build (chains._interval_mats_split: interval i's Van Loan
+    paths, propagator and group sums on rank i mod world, one all-gather) gives every rank
+    the single-rank model; each rank evaluates only its own intervals' paths."""
+    import torch.multiprocessing as mp
+    from helpers.torch_linalg import FakeTorchLinalg
+    from itrails_amd.model import trans_emiss_calc
+    g = golden("model_kat_3_3.npz")
+    la = FakeTorchLinalg()
+    a1, _, pi1, _, _ = trans_emiss_calc(*g["args"], 3, 3, la=la)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_build_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for _, a, pi, _ in res:
+        assert np.array_equal(a, a1) and np.array_equal(pi, pi1)
+    assert sum(v for _, _, _, v in res) == la.stats["vanloan"]

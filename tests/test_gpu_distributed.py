@@ -98,3 +98,50 @@ def test_bench_self_launch_two_ranks(gpu):
     assert r["scaling"] == "strong" and r["config"]["columns_total"] == 3_000_000
     assert r["viterbi_equal"] is True and r["columns_checked"] == 3_000_000
     assert r["loglik_max_rel_err"] < 1e-8
+
+
+def _split_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    try:
+        from itrails_amd.model import trans_emiss_calc
+        from itrails_amd.model.linalg import DeviceLinalg, split_build
+        g = golden("model_kat_5_5.npz")
+        with split_build(True):
+            la = DeviceLinalg()
+            a, b, pi, _, _ = trans_emiss_calc(*g["args"], 5, 5, la=la)
+        q.put((rank, a, pi, la.stats["vanloan"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_split_model_build_two_ranks_matches_single_rank(gpu):
+    """The rank-split (5,5) model build on the real HIP path (two gloo ranks on cuda:0):
+    each rank evaluates half of the intervals' Van Loan paths, the all-gather shares them,
+    and every rank's model equals the single-rank build bit for bit (and the reference's
+    within the model tolerance)."""
+    import torch.multiprocessing as mp
+    from itrails_amd.model import trans_emiss_calc
+    from itrails_amd.model.linalg import DeviceLinalg
+    g = golden("model_kat_5_5.npz")
+    la = DeviceLinalg()
+    a1, _, pi1, _, _ = trans_emiss_calc(*g["args"], 5, 5, la=la)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for _, a, pi, _ in res:
+        assert np.array_equal(a, a1) and np.array_equal(pi, pi1)
+        assert np.allclose(a, g["a"], rtol=1e-10, atol=1e-15)
+    assert sum(v for _, _, _, v in res) == la.stats["vanloan"]

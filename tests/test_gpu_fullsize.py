@@ -104,6 +104,31 @@ def test_full_size_posterior_rows(full):
     torch.cuda.empty_cache()
 
 
+def test_full_size_posterior_split_matches_unsplit(full, monkeypatch):
+    """The posterior's concurrent forward/backward split (the longest blocks' backward
+    sweeps run beside the forward sweep, post_combine_kernel joins the stored rows) against
+    the two-pass sweep (ITR_POST_SPLIT_FRAC=0 at plan creation) on every row, and the
+    longest blocks against the CPU restatement."""
+    import torch
+    n = full["a"].shape[0]
+    plan = hmm.Plan(full["off"])
+    plan.reserve(n, posterior=True)
+    post = hmm.posterior_device(full["model"], plan, full["d_obs"])
+    monkeypatch.setenv("ITR_POST_SPLIT_FRAC", "0")
+    plan0 = hmm.Plan(full["off"])
+    plan0.reserve(n, posterior=True)
+    post0 = hmm.posterior_device(full["model"], plan0, full["d_obs"])
+    assert float((post - post0).abs().max()) < 1e-12
+    del post0, plan0
+    obs, off, k = full["obs"], full["off"], np.sort(full["longest"][:3])
+    so, soff = _sub(obs, off, k)
+    ref = O.posterior(full["t"], so, soff)
+    rows = torch.cat([post[off[b]:off[b + 1]] for b in k]).cpu().numpy()
+    np.testing.assert_allclose(rows, ref, rtol=1e-8, atol=1e-300)
+    del post
+    torch.cuda.empty_cache()
+
+
 def test_full_size_posterior_host_copy(full):
     """post_prob_wrapper from host blocks (itr_posterior_host: 5.6 GB of rows returned
     through the chunked pinned-staging copy) equals the device-resident posterior bit for
