@@ -63,8 +63,12 @@ struct PairGemmArgs {
 // XCD b % 8: logical tile ids are dealt so that the tiles of one member (which read the same
 // X and Y blocks) land on the same XCD and share its L2.
 __global__ void __launch_bounds__(256) pair_gemm_kernel(PairGemmArgs g) {
-  __shared__ double As[TK][TT + 2];
-  __shared__ double Bs[TK][TT + 2];
+  // A tile kept row-major (m, k) with a pitch of 17 doubles and the B tile (k, n) with a
+  // pitch of 80: the MFMA operand reads (16 lanes along m or n, the next 16 lanes one k
+  // further) then hit 32 distinct bank pairs per half-wave — no LDS bank conflicts
+  constexpr int PA = TK + 1, PB = TT + 16;
+  __shared__ double As[TT * PA];
+  __shared__ double Bs[TK * PB];
   const int tiles = g.tn * g.tn;
   const int64_t total = g.nout * tiles;
   const int64_t per = gridDim.x >> 3;
@@ -96,9 +100,13 @@ __global__ void __launch_bounds__(256) pair_gemm_kernel(PairGemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
 
+  // A: lane -> row tid/4, four consecutive k (32 B per lane); B: lane -> column tid % 64,
+  // k rows w, w+4, w+8, w+12 (a wave reads 512 contiguous bytes of one row and its 16-lane
+  // store groups cover 32 distinct banks)
+  constexpr int RA = TT * TK / 256 / 4, RB = TK * TT / 256;
   const int ar = tid >> 2, ak = (tid & 3) * 4;
-  const int bk = tid >> 4, bc = (tid & 15) * 4;
-  double ra[4], rb[4];
+  const int bcol = tid & 63;
+  double ra[4 * RA], rb[RB];
   auto fetch = [&](int step) {
     const int pr = p0 + step / ksteps;
     const int k0 = (step % ksteps) * TK;
@@ -106,33 +114,36 @@ __global__ void __launch_bounds__(256) pair_gemm_kernel(PairGemmArgs g) {
     const double* __restrict__ B = g.Y + (int64_t)g.py[pr] * nn;
     const int gr = row0 + ar;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int gk = k0 + ak + e;
-      ra[e] = (gr < nb && gk < nb) ? A[(int64_t)gr * nb + gk] : 0.0;
-    }
-    const int gk = k0 + bk;
+    for (int h = 0; h < RA; ++h)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int gc = col0 + bc + e;
+      for (int e = 0; e < 4; ++e) {
+        const int gk = k0 + h * 16 + ak + e;
+        ra[4 * h + e] = (gr < nb && gk < nb) ? A[(int64_t)gr * nb + gk] : 0.0;
+      }
+    const int gc = col0 + bcol;
+#pragma unroll
+    for (int e = 0; e < RB; ++e) {
+      const int gk = k0 + w + 4 * e;
       rb[e] = (gk < nb && gc < nb) ? B[(int64_t)gk * nb + gc] : 0.0;
     }
   };
   if (nsteps > 0) fetch(0);
   for (int step = 0; step < nsteps; ++step) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      As[ak + e][ar] = ra[e];
-      Bs[bk][bc + e] = rb[e];
-    }
+    for (int h = 0; h < RA; ++h)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) As[ar * PA + h * 16 + ak + e] = ra[4 * h + e];
+#pragma unroll
+    for (int e = 0; e < RB; ++e) Bs[(w + 4 * e) * PB + bcol] = rb[e];
     __syncthreads();
     if (step + 1 < nsteps) fetch(step + 1);
 #pragma unroll
     for (int kk = 0; kk < TK; kk += 4) {
       double a[2], b[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = As[kk + (l >> 4)][wr * 32 + i * 16 + (l & 15)];
+      for (int i = 0; i < 2; ++i) a[i] = As[(wr * 32 + i * 16 + (l & 15)) * PA + kk + (l >> 4)];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = Bs[kk + (l >> 4)][wc * 32 + j * 16 + (l & 15)];
+      for (int j = 0; j < 2; ++j) b[j] = Bs[(kk + (l >> 4)) * PB + wc * 32 + j * 16 + (l & 15)];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll

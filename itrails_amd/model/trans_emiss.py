@@ -11,7 +11,8 @@ from __future__ import annotations
 
 import numpy as np
 
-from .chains import joint_prob_mat
+from .chains import joint_prob_mat, prefetch_vanloan
+from .statespace import state_space
 from .emissions import cutpoints_AB, cutpoints_ABC, emission_rows, state_specs
 
 _NT = ["A", "C", "T", "G"]
@@ -45,11 +46,17 @@ def trans_emiss_calc(t_A, t_B, t_C, t_2, t_upper, t_out, N_AB, N_ABC, r, n_int_A
             raise ValueError(f"unknown cutpoint scheme {cut_ABC!r}")
         cut_ABC = cutpoints_ABC(n_int_ABC, coal_ABC)
 
-    J = joint_prob_mat(t_A, t_B, t_AB, t_C, rho, rho, rho, rho, rho, coal_AB, coal_AB,
-                       coal_AB, coal_AB, coal_ABC, n_int_AB, n_int_ABC, cut_AB, cut_ABC, la=la)
+    # the three-species chain's Van Loan work (the bulk of the build's device time) starts
+    # first, on a side stream, and runs while the host builds the emission tables and the
+    # two-species chain
+    prefetch_vanloan(state_space(3).rate_matrix(coal_ABC, rho),
+                     [cut_ABC[i + 1] - cut_ABC[i] for i in range(len(cut_ABC) - 1)],
+                     state_space(3), n_int_ABC, la)
     specs = state_specs(t_A, t_B, t_AB, t_C, t_upper, t_out, coal_AB, coal_ABC, n_int_AB,
                         n_int_ABC, mu, mu, mu, mu, mu, mu, cut_AB, cut_ABC)
     states, rows = emission_rows(specs, la=la)
+    J = joint_prob_mat(t_A, t_B, t_AB, t_C, rho, rho, rho, rho, rho, coal_AB, coal_AB,
+                       coal_AB, coal_AB, coal_ABC, n_int_AB, n_int_ABC, cut_AB, cut_ABC, la=la)
     order = sorted(range(len(states)), key=lambda i: states[i])
     hidden = [states[i] for i in order]
     b = rows[order]

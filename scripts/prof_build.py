@@ -54,6 +54,25 @@ def main():
     t0 = time.perf_counter()
     ev(50)
     print(f"instrumented build {time.perf_counter() - t0:.3f} s")
+    # host-side cost of the Van Loan call (planning + launches, no synchronisation)
+    from itrails_amd.model import linalg as LA
+    orig = LA.DeviceLinalg.vanloan_batch
+    hs = []
+
+    def vb(self, *a, **k):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        r = orig(self, *a, **k)
+        hs.append(time.perf_counter() - t1)
+        return r
+    LA.DeviceLinalg.vanloan_batch = vb
+    for i in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev(60 + i)
+        torch.cuda.synchronize()
+        print(f"build {time.perf_counter() - t0:.4f} s, vanloan host enqueue {hs[-1] * 1e3:.2f} ms")
+    LA.DeviceLinalg.vanloan_batch = orig
     agg = {}
     for name, shp, kb, t in log:
         k = (name, shp, kb)
