@@ -669,10 +669,31 @@ def _evaluate(P: _ABCPlan, cut, Q, om, tab, tab_names, la):
     by_k: Dict[int, List[Tuple]] = {}
     for path, k in vl:
         by_k.setdefault(k, []).append(path)
-    for k, paths in sorted(by_k.items()):
-        res = la.vanloan(Q, cut[k + 1] - cut[k], masks, paths)
-        for p, m in zip(paths, res):
-            vl[(p, k)] = m
+    if by_k and hasattr(la, "vanloan_batch"):
+        # every interval's Van Loan paths in one shared evaluation (one job per interval)
+        keys = list(masks)
+        mid = {kk: i for i, kk in enumerate(keys)}
+        mu8 = np.stack([np.asarray(masks[kk], dtype=np.uint8) for kk in keys])
+        ks = sorted(by_k)
+        job, lens, pm, owner = [], [], [], []
+        for j, k in enumerate(ks):
+            for path in by_k[k]:
+                job.append(j)
+                lens.append(len(path))
+                pm.extend(mid[w] for w in path)
+                owner.append((path, k))
+        off = np.zeros(len(job) + 1, dtype=np.int64)
+        np.cumsum(lens, out=off[1:])
+        t = np.asarray([cut[k + 1] - cut[k] for k in ks], dtype=np.float64)
+        res = la.vanloan_batch(Q, mu8, t, np.asarray(job, dtype=np.int32), off,
+                               np.asarray(pm, dtype=np.int32)).cpu().numpy()
+        for key, m in zip(owner, res):
+            vl[key] = m
+    else:
+        for k, paths in sorted(by_k.items()):
+            res = la.vanloan(Q, cut[k + 1] - cut[k], masks, paths)
+            for p, m in zip(paths, res):
+                vl[(p, k)] = m
     if inf:
         paths = list(inf)
         res = la.deepest(Q[:nt, :nt], masks_t, paths)
