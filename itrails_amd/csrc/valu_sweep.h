@@ -708,13 +708,15 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
                 for (int r = 0; r < RJN; ++r)
                   if (jv[r]) p.alpha[rec + jr[r]] = x[r];
               }
-              if ((sub == TE - 1 || t == T - 1) && q == 0) {  // the tile's flag words
-#pragma unroll
-                for (int r = 0; r < RJN; ++r)
-                  if (jv[r]) p.stay[rec + jr[r]] = (uint16_t)bits[r];
-              }
               STAMP(5);
             }
+          }
+          // the tile's flag words, once per tile (bits of columns past the block's end are
+          // never read by the traceback)
+          if (q == 0) {
+#pragma unroll
+            for (int r = 0; r < RJN; ++r)
+              if (jv[r]) p.stay[rec + jr[r]] = (uint16_t)bits[r];
           }
         }
         // last state = first argmax of omega_{T-1}  (optimizer.py:346)
