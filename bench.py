@@ -275,6 +275,9 @@ def main():
                     help="columns of the 1-core CPU-baseline sample (0 = skip)")
     ap.add_argument("--host-path", type=int, default=1,
                     help="1: also time the drop-in wrappers on host NumPy buffers (N = 1)")
+    ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
+                    help="fv mode: 1 = one itr_forward_viterbi call per step (forward sweep "
+                         "beside the Viterbi sweep's longest blocks); 0 = the two calls in turn")
     ap.add_argument("--split-build", type=int, default=1, choices=[0, 1],
                     help="optimize mode, N > 1: divide each rebuild's Van Loan work over the "
                          "ranks (one RCCL all-gather) instead of rebuilding on every rank")
@@ -335,7 +338,7 @@ def main():
     d_post = torch.empty((plan.total, n), dtype=torch.float64, device=dev) if post_mode else None
     d_ll_global = torch.zeros(W["nblocks"], dtype=torch.float64, device=cdev)
 
-    fwd_ms, vit_ms, tb_ms, build_ms = [], [], [], []
+    fwd_ms, vit_ms, tb_ms, build_ms, fv_ms = [], [], [], [], []
     eval_no = [0]
 
     def exchange():
@@ -385,6 +388,12 @@ def main():
                 fwd_ms.append(hmm.last_kernel_ms("posterior_fwd"))
                 vit_ms.append(hmm.last_kernel_ms("posterior_bwd"))
             return
+        if args.overlap and not timing:
+            # forward + Viterbi in one call (itr_forward_viterbi): the forward sweep runs
+            # beside the Viterbi sweep's longest blocks on a disjoint set of CUs
+            hmm.forward_viterbi_device(model, plan, d_obs, out_ll=d_ll, out_path=d_path)
+            exchange()
+            return
         hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
         if timing:
             fwd_ms.append(hmm.last_kernel_ms("forward"))
@@ -393,6 +402,9 @@ def main():
         if timing:
             vit_ms.append(hmm.last_kernel_ms("viterbi"))
             tb_ms.append(hmm.last_kernel_ms("traceback"))
+            if args.overlap:
+                hmm.forward_viterbi_device(model, plan, d_obs, out_ll=d_ll, out_path=d_path)
+                fv_ms.append(hmm.last_kernel_ms("forward_viterbi"))
 
     for _ in range(args.warmup):
         step()
@@ -555,6 +567,7 @@ def main():
                          "forward_ms": round(fwd_avg, 4),
                          "viterbi_ms": round(vit_avg, 4) if args.mode == "fv" else None,
                          "traceback_ms": round(tb_avg, 4) if args.mode == "fv" else None,
+                         "forward_viterbi_ms": round(float(np.mean(fv_ms)), 4) if fv_ms else None,
                          "algorithmic": f"{pair_ops:.0f} FP64 ops/column per sweep x "
                                         f"{cols_local} columns (rank 0)",
                          "step_ideal_ms": round(ideal_ms, 4),

@@ -106,6 +106,13 @@ ITR_API int itr_forward_loglik(itr_model_t model, itr_plan_t plan, const uint16_
 ITR_API int itr_viterbi(itr_model_t model, itr_plan_t plan, const uint16_t* d_obs,
                         uint8_t* d_path, void* stream);
 
+/* itr_forward_loglik and itr_viterbi in one call (the same outputs, bit for bit), the
+ * forward sweep overlapped with the Viterbi sweep's longest blocks on a disjoint set of CUs.
+ * For a caller that needs both over the same alignment (e.g. scoring a model and decoding
+ * with it: loglik_wrapper then viterbi_wrapper, optimizer.py:40-65, 357-377). */
+ITR_API int itr_forward_viterbi(itr_model_t model, itr_plan_t plan, const uint16_t* d_obs,
+                                double* d_loglik, uint8_t* d_path, void* stream);
+
 /* Posterior decoding.
  * Replaces post_prob (optimizer.py:216-238) including the reference's backward recursion
  * beta_t = (beta_{t+1} * e_{t+1}) @ a (optimizer.py:207-212): d_post is (total_columns x N)

@@ -38,6 +38,7 @@ _SIGNATURES = {
     "itr_plan_reserve": ([_P, _I, _I], _I),
     "itr_forward_loglik": ([_P, _P, _P, _P, _P], _I),
     "itr_viterbi": ([_P, _P, _P, _P, _P], _I),
+    "itr_forward_viterbi": ([_P, _P, _P, _P, _P, _P], _I),
     "itr_posterior": ([_P, _P, _P, _P, _P], _I),
     "itr_pack_symbols": ([_P, _P, _I64, _P, _P], _I),
     "itr_forward_loglik_host": ([_P, _P, _P, _P], _I),

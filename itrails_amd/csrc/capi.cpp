@@ -6,8 +6,10 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <numeric>
+#include <optional>
 #include <atomic>
 #include <string>
 #include <thread>
@@ -93,6 +95,44 @@ int cu_count() {
   return n > 0 ? n : 256;
 }
 
+// Two CU-masked streams per device and host thread: `lng` on `reserve` CUs spread over the
+// device, `blk` on the others, plus fork / join events.  itr_viterbi decodes the longest
+// blocks on `lng` with the 9-wave VALU layout (one workgroup per CU, lowest step latency)
+// while everything else runs on `blk`; the masks keep the two launches off each other's CUs
+// whatever order the dispatcher takes them in.
+struct Partition {
+  int device = -1, reserve = 0;
+  hipStream_t lng = nullptr, blk = nullptr;
+  hipEvent_t fork = nullptr, jl = nullptr, jb = nullptr;
+};
+thread_local std::vector<Partition> g_parts;
+
+int partition(int reserve, Partition** out) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  for (auto& x : g_parts)
+    if (x.device == dev && x.reserve == reserve) {
+      *out = &x;
+      return 0;
+    }
+  const int cus = cu_count();
+  std::vector<uint32_t> ml((cus + 31) / 32, 0u), mb((cus + 31) / 32, 0u);
+  std::vector<char> in(cus, 0);
+  for (int k = 0; k < reserve; ++k) in[(int)((int64_t)k * cus / reserve)] = 1;
+  for (int c = 0; c < cus; ++c) (in[c] ? ml : mb)[c / 32] |= 1u << (c % 32);
+  Partition x;
+  x.device = dev;
+  x.reserve = reserve;
+  HIP_TRY(hipExtStreamCreateWithCUMask(&x.lng, (uint32_t)ml.size() * 32, ml.data()));
+  HIP_TRY(hipExtStreamCreateWithCUMask(&x.blk, (uint32_t)mb.size() * 32, mb.data()));
+  HIP_TRY(hipEventCreateWithFlags(&x.fork, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&x.jl, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&x.jb, hipEventDisableTiming));
+  g_parts.push_back(x);
+  *out = &g_parts.back();
+  return 0;
+}
+
 template <class T>
 int dev_alloc(T** p, size_t count) {
   *p = nullptr;
@@ -113,6 +153,10 @@ struct itr_model {
   int n = 0;
   double *a = nullptr, *la = nullptr, *E = nullptr, *LE = nullptr, *PIE = nullptr,
          *LPIE = nullptr, *aT = nullptr;
+  // log E with rows padded to the one-block-per-wave Viterbi layout's width (-inf columns),
+  // when that layout serves this state count (wave_vit.hip)
+  double* LEW = nullptr;
+  int xrw = 0;
 };
 
 struct itr_plan {
@@ -177,6 +221,12 @@ int check_plan(itr_plan_t p) {
 // Workspace: Viterbi = one checkpoint row (f64) and one flag word (u16) per state per
 // 16-column tile record; posterior = the forward rows of every column.
 int vit_stride(int n) {  // record stride of the Viterbi workspace for this state count
+  const itr::WaveVitGeometry wv = itr::wave_vit_geometry(n);
+  bool wave = wv.iq > 0;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_NO_WAVE")) wave = false;
+#endif
+  if (wave) return wv.xr;
   const itr::VitHybridGeometry vh = itr::vit_hybrid_geometry(n);
   return vh.cfg >= 0 ? vh.xr : itr::sweep_row_stride(n, itr::MODE_VIT);
 }
@@ -231,12 +281,15 @@ itr::SweepArgs base_args(itr_model_t m, itr_plan_t p, const uint16_t* obs) {
 uint64_t* g_diag = nullptr;  // diagnostic build: per-segment cycle sums of the last sweep
 #endif
 
-int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname) {
+// tname: kernel timer (nullptr: none); max_grid > 0 caps the persistent grid
+int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
+              int64_t max_grid = -1) {
   itr::SweepGeometry g = itr::sweep_geometry(a.n, mode);
   if (g.iq < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", a.n);
   a.xp = g.xp;
   int64_t grid = (int64_t)g.per_cu * cu_count();
   if (grid > a.nblocks) grid = a.nblocks;
+  if (max_grid > 0 && grid > max_grid) grid = max_grid;
   if (grid <= 0) return 0;
   if (grid <= cu_count()) g.lds = std::max(g.lds, itr::kExclusiveLds);  // one per CU
   HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
@@ -249,8 +302,10 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname) {
   a.diag = g_diag;
   a.diag_wave = getenv("ITR_DIAG_WAVE") ? atoi(getenv("ITR_DIAG_WAVE")) : 0;
 #endif
-  {
+  if (tname) {
     Scope sc(tname, st);
+    HIP_TRY(itr::launch_sweep(mode, g, (int)grid, a, st));
+  } else {
     HIP_TRY(itr::launch_sweep(mode, g, (int)grid, a, st));
   }
   return 0;
@@ -364,6 +419,22 @@ int itr_model_create(int n, const double* a, const double* la, const double* E,
     itr_model_destroy(m);
     return e;
   }
+  const itr::WaveVitGeometry wv = itr::wave_vit_geometry(n);
+  if (wv.iq > 0) {
+    const int w = wv.xr;
+    std::vector<double> lew((size_t)ITR_NOBS * w, -INFINITY);
+    for (int o = 0; o < ITR_NOBS; ++o)
+      for (int j = 0; j < n; ++j) lew[(size_t)o * w + j] = LE[(size_t)o * n + j];
+    e = dev_alloc(&m->LEW, lew.size());
+    if (!e && hipMemcpy(m->LEW, lew.data(), lew.size() * sizeof(double),
+                        hipMemcpyHostToDevice) != hipSuccess)
+      e = fail(ITR_EHIP, "table upload failed");
+    if (e) {
+      itr_model_destroy(m);
+      return e;
+    }
+    m->xrw = w;
+  }
   *out = m;
   return 0;
 }
@@ -377,6 +448,7 @@ int itr_model_destroy(itr_model_t m) {
   dev_free(m->PIE);
   dev_free(m->LPIE);
   dev_free(m->aT);
+  dev_free(m->LEW);
   delete m;
   return 0;
 }
@@ -679,14 +751,17 @@ int itr_forward_loglik(itr_model_t m, itr_plan_t p, const uint16_t* obs, double*
   return 0;
 }
 
-int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
-                void* stream) {
-  if (int e = check_model(m)) return e;
-  if (int e = check_plan(p)) return e;
-  if (p->nblocks == 0 || p->total == 0) return 0;
-  if (!obs || !path) return fail(ITR_EINVAL, "null device pointer");
+}  // extern "C"
+
+namespace {
+
+// The Viterbi sweep and traceback of every block into `path`; with fwd_loglik, the forward
+// log-likelihood sweep too, overlapped with the Viterbi sweep's longest blocks.
+int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
+                 hipStream_t st, double* fwd_loglik) {
   if (int e = reserve(p, m->n, true, false)) return e;
-  hipStream_t st = (hipStream_t)stream;
+  std::optional<Scope> both;  // the combined call's timer: fork to join, traceback excluded
+  if (fwd_loglik) both.emplace("forward_viterbi", st);
   itr::SweepArgs a = base_args(m, p, obs);
   a.mat = m->la;
   a.emit = m->LE;
@@ -695,8 +770,80 @@ int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
   a.alpha = p->d_alpha;
   a.stay = p->d_stay;
   a.last_state = p->d_last;
+  const itr::WaveVitGeometry wv = itr::wave_vit_geometry(m->n);
   const itr::VitHybridGeometry vh = itr::vit_hybrid_geometry(m->n);
-  if (vh.cfg >= 0) {
+  bool wave = wv.iq > 0 && m->LEW && m->xrw == wv.xr;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_NO_WAVE")) wave = false;
+#endif
+  if (!wave && fwd_loglik)  // no overlap: the forward sweep first, on the caller's stream
+    if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, st)) return e;
+  if (wave) {
+    // The longest blocks (longest first, while longer than lfrac x the longest and while
+    // their columns fit `reserve` CUs for the longest block's duration) on the 9-wave VALU
+    // layout on the reserved CUs; the rest one block per wavefront on the other CUs.
+    const int cus = cu_count();
+    int reserve_cus = cus / 5;
+    double lfrac = 0.3;
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_VIT_RESERVE")) reserve_cus = atoi(getenv("ITR_VIT_RESERVE"));
+    if (getenv("ITR_VIT_LONG_FRAC")) lfrac = atof(getenv("ITR_VIT_LONG_FRAC"));
+#endif
+    reserve_cus = std::max(1, std::min(reserve_cus, cus - 1));
+    const int64_t tmax = p->sorted_len[0];
+    int64_t nlong = 0, cum = 0;
+    while (nlong < p->nblocks && p->sorted_len[nlong] >= 2048 &&
+           (double)p->sorted_len[nlong] > lfrac * (double)tmax &&
+           cum + p->sorted_len[nlong] <= (int64_t)reserve_cus * tmax) {
+      cum += p->sorted_len[nlong];
+      ++nlong;
+    }
+    itr::VitArgs w{};
+    w.n = m->n;
+    w.xr = wv.xr;
+    w.nblocks = p->nblocks - nlong;
+    w.order = p->d_order + nlong;
+    w.queue = p->d_queue + 7;
+    w.off = p->d_off;
+    w.tile_off = p->d_tile_off;
+    w.obs = obs;
+    w.la = m->la;
+    w.lew = m->LEW;
+    w.lpie = m->LPIE;
+    w.ckpt = p->d_alpha;
+    w.stay = p->d_stay;
+    w.last_state = p->d_last;
+    // the bulk's longest blocks (about one per SIMD pair) at raised wave priority
+    w.prio_len = (int)std::max<int64_t>(1, p->sorted_len[std::min<int64_t>(p->nblocks - 1,
+                                                                          nlong + cus / 2)]);
+    std::optional<Scope> sc;
+    if (!fwd_loglik) sc.emplace("viterbi", st);
+    Partition* pt = nullptr;
+    if (nlong > 0) {
+      if (int e = partition(reserve_cus, &pt)) return e;
+      HIP_TRY(hipEventRecord(pt->fork, st));
+      HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
+      HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
+      a.nblocks = nlong;
+      if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, reserve_cus)) return e;
+    }
+    hipStream_t sb = pt ? pt->blk : st;
+    if (fwd_loglik)
+      if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, sb)) return e;
+    if (w.nblocks > 0) {
+      const int64_t work = (w.nblocks + 3) / 4;
+      const int64_t grid =
+          std::min<int64_t>((int64_t)wv.per_cu * (cus - (pt ? reserve_cus : 0)), work);
+      HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), sb));
+      HIP_TRY(itr::launch_wave_vit(wv, (int)grid, w, sb));
+    }
+    if (pt) {
+      HIP_TRY(hipEventRecord(pt->jl, pt->lng));
+      HIP_TRY(hipEventRecord(pt->jb, pt->blk));
+      HIP_TRY(hipStreamWaitEvent(st, pt->jl, 0));
+      HIP_TRY(hipStreamWaitEvent(st, pt->jb, 0));
+    }
+  } else if (vh.cfg >= 0) {
     // the longest blocks (longer than vfrac x the longest) as VALU tasks, the rest in
     // lock-step groups; one workgroup per CU
     double vfrac = 0.35;
@@ -724,6 +871,7 @@ int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
 #endif
     if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
   }
+  both.reset();
   itr::TraceArgs ta{};
   ta.n = m->n;
   ta.xr = vit_stride(m->n);
@@ -745,6 +893,29 @@ int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
   Scope sc("traceback", st);
   HIP_TRY(itr::launch_vit_traceback(ta, (int)grid, st));
   return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int itr_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
+                void* stream) {
+  if (int e = check_model(m)) return e;
+  if (int e = check_plan(p)) return e;
+  if (p->nblocks == 0 || p->total == 0) return 0;
+  if (!obs || !path) return fail(ITR_EINVAL, "null device pointer");
+  return viterbi_impl(m, p, obs, path, (hipStream_t)stream, nullptr);
+}
+
+int itr_forward_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* loglik,
+                        uint8_t* path, void* stream) {
+  if (int e = check_model(m)) return e;
+  if (int e = check_plan(p)) return e;
+  if (p->nblocks == 0) return 0;
+  if (!obs || !path || !loglik) return fail(ITR_EINVAL, "null device pointer");
+  if (p->total == 0) return itr_forward_loglik(m, p, obs, loglik, stream);
+  return viterbi_impl(m, p, obs, path, (hipStream_t)stream, loglik);
 }
 
 int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post,

@@ -132,6 +132,35 @@ VitHybridGeometry vit_hybrid_geometry(int n);
 hipError_t launch_vit_hybrid(const VitHybridGeometry& g, int grid, const SweepArgs& v, int nurg,
                              int* cu_busy, hipStream_t st);
 
+// Viterbi with one block per wavefront (wave_vit.hip)
+struct VitArgs {
+  int n;                        // hidden states
+  int xr;                       // record stride of the checkpoint rows / flag words
+  int64_t nblocks;              // blocks of `order`
+  const int32_t* order;         // [nblocks] longest first
+  int* queue;                   // work counter, zero at launch
+  const int64_t* off;           // [plan blocks + 1]
+  const int64_t* tile_off;      // [plan blocks + 1]
+  const uint16_t* obs;          // [total]
+  const double* la;             // log a, n x n
+  const double* lew;            // log E, 625 x xr (columns >= n: -inf)
+  const double* lpie;           // log(pi E), 625 x n
+  double* ckpt;                 // [tiles x xr]
+  uint16_t* stay;               // [tiles x xr]
+  uint8_t* last_state;          // [plan blocks]
+  int prio_len;                 // blocks at least this long run at raised wave priority
+};
+struct WaveVitGeometry {
+  int iq;       // sources (= targets) per lane chunk; negative: no wave layout for this n
+  int block;    // threads per workgroup
+  int xr;       // padded targets (8 iq): record stride and log-emission table width
+  size_t lds;   // dynamic LDS bytes
+  int per_cu;   // resident workgroups per CU
+};
+WaveVitGeometry wave_vit_geometry(int n);
+hipError_t launch_wave_vit(const WaveVitGeometry& g, int grid, const VitArgs& p,
+                           hipStream_t st);
+
 // log-likelihoods of the split blocks of a forward sweep
 hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,
                                     const double* svec, const int* sK, double* loglik,

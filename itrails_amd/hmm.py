@@ -179,6 +179,19 @@ def viterbi_device(model: Model, plan: Plan, d_obs, out=None):
     return out
 
 
+def forward_viterbi_device(model: Model, plan: Plan, d_obs, out_ll=None, out_path=None):
+    """forward_loglik_device and viterbi_device in one call (identical outputs), the forward
+    sweep overlapped with the Viterbi sweep's longest blocks (itr_forward_viterbi)."""
+    import torch
+
+    _check_obs(plan, d_obs)
+    out_ll = _out(out_ll, (plan.nblocks,), torch.float64, d_obs.device)
+    out_path = _out(out_path, (plan.total,), torch.uint8, d_obs.device)
+    check(lib().itr_forward_viterbi(model.handle, plan.handle, ptr(d_obs), ptr(out_ll),
+                                    ptr(out_path), _stream_handle()))
+    return out_ll, out_path
+
+
 def posterior_device(model: Model, plan: Plan, d_obs, out=None):
     """Posterior state probabilities (float64 [total, N])."""
     import torch

@@ -5,4 +5,5 @@ import sys
 d = json.load(open(sys.argv[1]))
 r = d["roofline"]
 print(" ".join(sys.argv[2:]), round(d["value"] / 1e6, 1), "Mcol/s fwd", r.get("forward_ms"),
-      "vit", r.get("kernel_ms"), "trace", r.get("traceback_ms"), "check", d.get("check"))
+      "vit", r.get("kernel_ms"), "trace", r.get("traceback_ms"), "fv", r.get("forward_viterbi_ms"),
+      "ms/step", d.get("ms_per_step"), "check", d.get("check"))

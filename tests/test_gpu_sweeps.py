@@ -55,7 +55,7 @@ def test_golden_sweeps(gpu, name):
     np.testing.assert_allclose(post[g["post_rows"]], g["post"], rtol=RTOL, atol=1e-300)
 
 
-@pytest.mark.parametrize("n", [1, 4, 16, 17, 27, 64, 70, 96, 133, 150, 192])
+@pytest.mark.parametrize("n", [1, 4, 16, 17, 27, 64, 65, 70, 72, 96, 133, 150, 192])
 def test_random_vs_oracle(gpu, n):
     rng = np.random.default_rng(1000 + n)
     a, b, pi = random_hmm(rng, n)
@@ -139,7 +139,7 @@ def test_device_layer_matches_host_layer(gpu):
     assert hmm.last_kernel_ms("viterbi") > 0
 
 
-@pytest.mark.parametrize("n", [5, 70, 133, 192])
+@pytest.mark.parametrize("n", [5, 65, 70, 72, 133, 192])
 def test_viterbi_frequent_switches(gpu, n):
     """Weakly sticky transitions and sharp emissions: the path switches every few columns,
     so nearly every 16-column tile holds several clear stay flags and the traceback rebuilds
@@ -155,3 +155,27 @@ def test_viterbi_frequent_switches(gpu, n):
     assert (np.diff(ref.astype(np.int64)) != 0).mean() > 0.1  # the regime under test
     model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
     np.testing.assert_array_equal(hmm._paths(model, plan, obs), ref)
+
+
+@pytest.mark.parametrize("n", [46, 65, 70, 72])
+def test_forward_viterbi_call_matches_separate_calls(gpu, n):
+    """itr_forward_viterbi (forward sweep beside the Viterbi sweep's longest blocks on a
+    disjoint CU set) returns exactly what itr_forward_loglik and itr_viterbi return, and the
+    Viterbi path is the oracle's.  Blocks of 2,048+ columns go to the long-block launch."""
+    import torch
+
+    rng = np.random.default_rng(70 + n)
+    a, b, pi = random_hmm(rng, n)
+    lengths = [9000, 7000, 6000, 4000, 3000, 2500] + list(rng.integers(1, 1500, size=300))
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=n, p_n=0.02, p_gap=0.02)
+    t = build_tables(a, b, pi)
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).to(gpu)
+    ll1 = hmm.forward_loglik_device(model, plan, d_obs).cpu().numpy()
+    p1 = hmm.viterbi_device(model, plan, d_obs).cpu().numpy()
+    ll2, p2 = hmm.forward_viterbi_device(model, plan, d_obs)
+    ll2, p2 = ll2.cpu().numpy(), p2.cpu().numpy()
+    np.testing.assert_array_equal(ll2, ll1)
+    np.testing.assert_array_equal(p2, p1)
+    np.testing.assert_array_equal(p2, O.viterbi(t, obs, off))
+    np.testing.assert_allclose(ll2, O.forward_loglik(t, obs, off), rtol=RTOL, atol=0)
