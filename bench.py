@@ -415,6 +415,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+        if os.environ.get("BENCH_STEP_TIMES"):  # diagnostics only: per-step wall times
+            torch.cuda.synchronize()
+            print(f"step {(time.perf_counter() - t0) * 1e3:.3f} ms", file=sys.stderr)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

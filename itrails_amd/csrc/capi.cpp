@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <deque>
 #include <numeric>
 #include <optional>
 #include <atomic>
@@ -50,7 +51,7 @@ struct Timer {
   hipEvent_t a = nullptr, b = nullptr;
   bool armed = false;
 };
-thread_local std::vector<Timer> g_timers;
+thread_local std::deque<Timer> g_timers;  // stable addresses: nested Scopes hold Timer*
 
 Timer* timer(const char* name) {
   int dev = 0;
@@ -99,13 +100,16 @@ int cu_count() {
 // device, `blk` on the others, plus fork / join events.  itr_viterbi decodes the longest
 // blocks on `lng` with the 9-wave VALU layout (one workgroup per CU, lowest step latency)
 // while everything else runs on `blk`; the masks keep the two launches off each other's CUs
-// whatever order the dispatcher takes them in.
+// whatever order the dispatcher takes them in.  Three streams: with the caller's that is the
+// 4 hardware queues a process gets by default (GPU_MAX_HW_QUEUES); a fifth stream shares a
+// queue with another and serialises against it (measured: 10 -> 12.5 ms per forward+Viterbi).
 struct Partition {
   int device = -1, reserve = 0;
-  hipStream_t lng = nullptr, blk = nullptr;
-  hipEvent_t fork = nullptr, jl = nullptr, jb = nullptr;
+  hipStream_t lng = nullptr, lng2 = nullptr;  // the reserved CUs
+  hipStream_t blk = nullptr;                   // the other CUs
+  hipEvent_t fork = nullptr, jl = nullptr, jl2 = nullptr, jb = nullptr;
 };
-thread_local std::vector<Partition> g_parts;
+thread_local std::deque<Partition> g_parts;
 
 int partition(int reserve, Partition** out) {
   int dev = 0;
@@ -124,9 +128,11 @@ int partition(int reserve, Partition** out) {
   x.device = dev;
   x.reserve = reserve;
   HIP_TRY(hipExtStreamCreateWithCUMask(&x.lng, (uint32_t)ml.size() * 32, ml.data()));
+  HIP_TRY(hipExtStreamCreateWithCUMask(&x.lng2, (uint32_t)ml.size() * 32, ml.data()));
   HIP_TRY(hipExtStreamCreateWithCUMask(&x.blk, (uint32_t)mb.size() * 32, mb.data()));
   HIP_TRY(hipEventCreateWithFlags(&x.fork, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&x.jl, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&x.jl2, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&x.jb, hipEventDisableTiming));
   g_parts.push_back(x);
   *out = &g_parts.back();
@@ -173,7 +179,9 @@ struct itr_plan {
   double* d_beta = nullptr;
   size_t beta_cap = 0;
   int32_t* d_order = nullptr;
-  int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep
+  int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep,
+                           // [3, 4] hybrid sweeps, [5, 6] Viterbi hybrid, [7] per-wave Viterbi,
+                           // [8, 9] the idle loop of a split hybrid launch
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
   std::vector<int64_t> sorted_len;  // block lengths, longest first (processing order)
@@ -313,8 +321,12 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
 
 // Hybrid sweep (mfma_sweeps.hip): the plan's urgent VALU tasks (v.tasks / v.order, v.nblocks)
 // then its matrix-core groups, in one persistent launch.  g from itr::mfma_geometry.
+// valu / mfma: launch the VALU tasks / the matrix-core groups (both: one launch; one of them:
+// that part only, so the two can run on different CU sets); zero_queues: reset the two work
+// counters on `st` first (a split launch resets them once, before both parts).
 int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const itr::MfmaGeometry& g,
-               hipStream_t st, const char* tname) {
+               hipStream_t st, const char* tname, bool valu = true, bool mfma = true,
+               int64_t max_grid = -1, bool zero_queues = true) {
   itr::MfmaArgs a{};
   a.n = m->n;
   const bool ll = mode == itr::MODE_FWD_LL;
@@ -345,23 +357,35 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   a.prio_len = INT32_MAX;
   v.queue = p->d_queue + 3;
   v.prio_len = 0;  // every VALU task of the hybrid is a long block: raised wave priority
+  // a part launched alone takes the other part's loop through a counter of its own (the
+  // real counter belongs to the concurrent launch of that part)
+  if (!valu) {
+    v.nblocks = 0;
+    v.queue = p->d_queue + 8;
+  }
+  if (!mfma) {
+    a.ngroups = 0;
+    a.queue = p->d_queue + 9;
+  }
   const int64_t work = v.nblocks + (a.ngroups + g.gb - 1) / g.gb;
   int per_cu = g.per_cu;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_HYB_PER_CU")) per_cu = atoi(getenv("ITR_HYB_PER_CU"));
 #endif
   int64_t grid = std::min<int64_t>((int64_t)per_cu * cu_count(), work);
+  if (max_grid > 0) grid = std::min(grid, max_grid);
   if (grid <= 0) return 0;
   itr::MfmaGeometry gx = g;
   if (grid <= cu_count()) gx.lds_min = itr::kExclusiveLds;  // one workgroup per CU
-  HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
+  if (zero_queues) HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
 #ifdef ITR_DIAG
   if (getenv("ITR_VERBOSE"))
     fprintf(stderr, "[itr] %s hybrid: n=%d cfg=%d block=%d per_cu=%d grid=%lld valu=%lld groups=%lld\n",
             tname, a.n, g.cfg, g.block, g.per_cu, (long long)grid, (long long)v.nblocks,
             (long long)a.ngroups);
 #endif
-  Scope sc(tname, st);
+  std::optional<Scope> sc;
+  if (tname) sc.emplace(tname, st);
   HIP_TRY(itr::launch_hybrid_sweep(mode, gx, (int)grid, a, v, st));
   return 0;
 }
@@ -653,7 +677,9 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   if (!e && hipMemset(p->d_cubusy, 0, 4096 * sizeof(int)) != hipSuccess)
     e = fail(ITR_EHIP, "plan workspace init failed");
   if (!e) e = dev_alloc(&p->d_order, nblocks);
-  if (!e) e = dev_alloc(&p->d_queue, 8);
+  if (!e) e = dev_alloc(&p->d_queue, 16);
+  if (!e && hipMemset(p->d_queue, 0, 16 * sizeof(int)) != hipSuccess)
+    e = fail(ITR_EHIP, "plan workspace init failed");
   if (!e) e = dev_alloc(&p->d_sink, 64);
   if (!e) e = dev_alloc(&p->d_last, nblocks);
   auto up = [&](void* d, const void* h, size_t bytes) {
@@ -776,28 +802,34 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_NO_WAVE")) wave = false;
 #endif
-  if (!wave && fwd_loglik)  // no overlap: the forward sweep first, on the caller's stream
-    if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, st)) return e;
-  if (wave) {
-    // The longest blocks (longest first, while longer than lfrac x the longest and while
-    // their columns fit `reserve` CUs for the longest block's duration) on the 9-wave VALU
-    // layout on the reserved CUs; the rest one block per wavefront on the other CUs.
-    const int cus = cu_count();
-    int reserve_cus = cus / 5;
-    double lfrac = 0.3;
+  // The longest blocks (longer than lfrac x the longest, at least 2,048 columns) on the
+  // 9-wave VALU layout on `reserve_cus` reserved CUs; the rest one block per wavefront on the
+  // other CUs (a lone wave steps ~2x slower, so the per-wave sweep must not get blocks
+  // longer than ~half the longest).  When the long blocks do not fit the reserved CUs within
+  // the longest block's time (workloads of few, equally long blocks), every block goes to
+  // the 9-wave layout on all CUs.
+  const int cus = cu_count();
+  int reserve_cus = cus / 4;
+  double lfrac = 0.45;
 #ifdef ITR_EXPERIMENT
-    if (getenv("ITR_VIT_RESERVE")) reserve_cus = atoi(getenv("ITR_VIT_RESERVE"));
-    if (getenv("ITR_VIT_LONG_FRAC")) lfrac = atof(getenv("ITR_VIT_LONG_FRAC"));
+  if (getenv("ITR_VIT_RESERVE")) reserve_cus = atoi(getenv("ITR_VIT_RESERVE"));
+  if (getenv("ITR_VIT_LONG_FRAC")) lfrac = atof(getenv("ITR_VIT_LONG_FRAC"));
 #endif
-    reserve_cus = std::max(1, std::min(reserve_cus, cus - 1));
+  reserve_cus = std::max(1, std::min(reserve_cus, cus - 1));
+  int64_t nlong = 0;
+  if (wave) {
     const int64_t tmax = p->sorted_len[0];
-    int64_t nlong = 0, cum = 0;
+    int64_t cum = 0;
     while (nlong < p->nblocks && p->sorted_len[nlong] >= 2048 &&
-           (double)p->sorted_len[nlong] > lfrac * (double)tmax &&
-           cum + p->sorted_len[nlong] <= (int64_t)reserve_cus * tmax) {
+           (double)p->sorted_len[nlong] > lfrac * (double)tmax) {
       cum += p->sorted_len[nlong];
       ++nlong;
     }
+    if (cum > (int64_t)reserve_cus * tmax) wave = false;
+  }
+  if (!wave && fwd_loglik)  // no overlap: the forward sweep first, on the caller's stream
+    if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, st)) return e;
+  if (wave) {
     itr::VitArgs w{};
     w.n = m->n;
     w.xr = wv.xr;
@@ -819,17 +851,52 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     std::optional<Scope> sc;
     if (!fwd_loglik) sc.emplace("viterbi", st);
     Partition* pt = nullptr;
+    // with the forward sweep: its VALU tasks (the halves of the longest blocks, latency-bound)
+    // beside the Viterbi long blocks on the reserved CUs, its matrix-core groups on the others
+    const itr::MfmaGeometry gf = itr::mfma_geometry(m->n, itr::MODE_FWD_LL);
+    const bool split_fwd = fwd_loglik && nlong > 0 && gf.cfg >= 0 && p->ngroups_ll > 0 &&
+                           p->nutasks > 0 && p->nutasks < reserve_cus;
+    itr::SweepArgs af = base_args(m, p, obs);
+    af.mat = m->a;
+    af.matT = m->aT;
+    af.emit = m->E;
+    af.init = m->PIE;
+    af.loglik = fwd_loglik;
+    af.tasks = p->d_utasks;
+    af.nblocks = p->nutasks;
+    af.svec = p->d_svec;
+    af.sK = p->d_sK;
+    int64_t rf = 0;  // reserved CUs for the forward's VALU tasks
+    if (split_fwd) {
+      rf = std::min<int64_t>(p->nutasks, reserve_cus / 4);
+#ifdef ITR_EXPERIMENT
+      if (getenv("ITR_FWD_RESERVE")) rf = std::min<int64_t>(atoi(getenv("ITR_FWD_RESERVE")), reserve_cus - 1);
+#endif
+      HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
+      HIP_TRY(hipMemsetAsync(p->d_queue + 8, 0, 2 * sizeof(int), st));  // the idle loops' counters
+    }
     if (nlong > 0) {
       if (int e = partition(reserve_cus, &pt)) return e;
       HIP_TRY(hipEventRecord(pt->fork, st));
       HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
       HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
       a.nblocks = nlong;
-      if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, reserve_cus)) return e;
+      if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, reserve_cus - rf)) return e;
+      if (split_fwd) {
+        HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
+        if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, pt->lng2, nullptr, true, false,
+                               rf, false))
+          return e;
+      }
     }
     hipStream_t sb = pt ? pt->blk : st;
-    if (fwd_loglik)
+    if (split_fwd) {
+      if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, sb, nullptr, false, true,
+                             (int64_t)gf.per_cu * (cus - reserve_cus), false))
+        return e;
+    } else if (fwd_loglik) {
       if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, sb)) return e;
+    }
     if (w.nblocks > 0) {
       const int64_t work = (w.nblocks + 3) / 4;
       const int64_t grid =
@@ -842,7 +909,14 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       HIP_TRY(hipEventRecord(pt->jb, pt->blk));
       HIP_TRY(hipStreamWaitEvent(st, pt->jl, 0));
       HIP_TRY(hipStreamWaitEvent(st, pt->jb, 0));
+      if (split_fwd) {
+        HIP_TRY(hipEventRecord(pt->jl2, pt->lng2));
+        HIP_TRY(hipStreamWaitEvent(st, pt->jl2, 0));
+      }
     }
+    if (split_fwd)  // log P of the split blocks from their two halves
+      HIP_TRY(itr::launch_fwd_split_combine(m->n, gf.xr, (int)p->nhsplit, p->d_hsplit_blk,
+                                            p->d_svec, p->d_sK, fwd_loglik, st));
   } else if (vh.cfg >= 0) {
     // the longest blocks (longer than vfrac x the longest) as VALU tasks, the rest in
     // lock-step groups; one workgroup per CU

@@ -285,7 +285,7 @@ hipError_t ws_get(size_t dbytes, size_t hbytes, Ws** out) {
   Ws& w = g_ws[dev & 15];
   if (!w.done) {
     if ((e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming))) return e;
-  } else if ((e = hipEventSynchronize(w.done))) {  // the previous call's staging copy
+  } else if ((e = hipEventSynchronize(w.done))) {  // the previous call has finished
     return e;
   }
   if (dbytes > w.dbytes) {
@@ -636,7 +636,6 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
   int* ds = reinterpret_cast<int*>(dstage);
   const double* dd = reinterpret_cast<const double*>(ds + ints);
   if ((e = hipMemcpyAsync(dstage, hs, hbytes, hipMemcpyHostToDevice, st))) return e;
-  if ((e = hipEventRecord(ws->done, st))) return e;
 
   const int bx = (int)std::min<int64_t>((nn + 255) / 256, 64);
   {
@@ -719,7 +718,11 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
                        dim3(bx, (unsigned)std::min<int64_t>(65535, npaths - p0)), dim3(256), 0,
                        st, nb, Wb[3], Wb[2], ds + out_idx_at + p0, ds + out_sel_at + p0,
                        d_out + p0 * nn);
-  return hipGetLastError();
+  if ((e = hipGetLastError())) return e;
+  // the workspace and the staging buffer are free again once everything above has run: the
+  // next call (ws_get) waits for this, whichever stream it is issued on (the model build
+  // prefetches one evaluation on a side stream while others run on the main stream)
+  return hipEventRecord(ws->done, st);
 }
 
 }  // namespace itr
