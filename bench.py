@@ -278,6 +278,10 @@ def main():
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
                     help="fv mode: 1 = one itr_forward_viterbi call per step (forward sweep "
                          "beside the Viterbi sweep's longest blocks); 0 = the two calls in turn")
+    ap.add_argument("--stream", default="side", choices=["side", "default"],
+                    help="launch stream of the timed steps: a created stream (side) or the "
+                         "legacy default stream, which synchronises implicitly with every "
+                         "blocking stream")
     ap.add_argument("--split-build", type=int, default=1, choices=[0, 1],
                     help="optimize mode, N > 1: divide each rebuild's Van Loan work over the "
                          "ranks (one RCCL all-gather) instead of rebuilding on every rank")
@@ -300,6 +304,8 @@ def main():
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if args.stream == "side":  # every launch of this process on one created stream
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)

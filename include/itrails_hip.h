@@ -140,6 +140,9 @@ ITR_API int itr_posterior_host(itr_model_t model, itr_plan_t plan, const uint16_
  * per calling thread for large copy-outs, bound to the thread's current device and
  * recreated when it changes; this frees the calling thread's set. */
 ITR_API int itr_release_staging(void);
+/* itr_viterbi / itr_forward_viterbi keep three CU-masked streams (and four events) per
+ * calling thread and device; this destroys the calling thread's set. */
+ITR_API int itr_release_streams(void);
 
 /* Timing hook for benchmarks: average device duration (ms) of the dominant kernel of the
  * last sweep issued on this thread, measured with HIP events on the sweep's stream. */

@@ -6,6 +6,7 @@ every entry point raises, so a GPU run can never silently use host code.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import re
@@ -45,6 +46,7 @@ _SIGNATURES = {
     "itr_viterbi_host": ([_P, _P, _P, _P], _I),
     "itr_posterior_host": ([_P, _P, _P, _P], _I),
     "itr_release_staging": ([], _I),
+    "itr_release_streams": ([], _I),
     "itr_last_kernel_ms": ([ctypes.c_char_p, ctypes.POINTER(_D)], _I),
     "itr_expm_batched": ([_I, _I64, _P, _P, _P], _I),
     "itr_expm_batched_host": ([_I, _I64, _P, _P], _I),
@@ -99,6 +101,8 @@ def lib():
         f.argtypes = args
         f.restype = res
     _lib = L
+    # the CU-masked streams of itr_viterbi go before the HIP runtime is torn down
+    atexit.register(L.itr_release_streams)
     return L
 
 

@@ -1178,6 +1178,21 @@ int itr_posterior_host(itr_model_t m, itr_plan_t p, const uint16_t* h_obs, doubl
   return copy_out_large(h_post, y.p, bytes);
 }
 
+int itr_release_streams(void) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  for (auto& x : g_parts) {
+    (void)hipSetDevice(x.device);
+    for (hipStream_t* q : {&x.lng, &x.lng2, &x.blk})
+      if (*q) (void)hipStreamDestroy(*q);
+    for (hipEvent_t* v : {&x.fork, &x.jl, &x.jl2, &x.jb})
+      if (*v) (void)hipEventDestroy(*v);
+  }
+  g_parts.clear();
+  (void)hipSetDevice(dev);
+  return 0;
+}
+
 int itr_release_staging(void) {
   g_stage.release();
   itr::release_vanloan_workspace();

@@ -4,15 +4,14 @@ mkdir -p gpurun_out
 : > gpurun_out/fvvar.log
 run() {  # label, bench args, then env assignments
   label=$1; bargs=$2; shift 2
-  env ITR_LIB=itrails_amd/libitrails_hip_exp.so BENCH_STEP_TIMES=1 "$@" timeout -k 10 120 python bench.py --steps 12 --warmup 2 --verify 0 --cpu-1core-cols 0 --host-path 0 $bargs > gpurun_out/ws.json 2> gpurun_out/ws.err || { echo "FAIL $label" >> gpurun_out/fvvar.log; cat gpurun_out/fvvar.log; exit 1; }
+  env ITR_LIB=itrails_amd/libitrails_hip_exp.so "$@" timeout -k 10 120 python bench.py --steps 12 --warmup 2 --verify 0 --cpu-1core-cols 0 --host-path 0 $bargs > gpurun_out/ws.json 2> gpurun_out/ws.err || { echo "FAIL $label" >> gpurun_out/fvvar.log; cat gpurun_out/fvvar.log; exit 1; }
   python scripts/bench_line.py gpurun_out/ws.json "$label" >> gpurun_out/fvvar.log
   grep "^step" gpurun_out/ws.err | tr '\n' ' ' >> gpurun_out/fvvar.log; echo >> gpurun_out/fvvar.log
 }
-run besideA ""
-run besideB ""
-run serial "" ITR_FV_BESIDE=0
-run beside_pc2 "" ITR_WAVE_PER_CU=2
-run beside_f16 "" ITR_FWD_RESERVE=16
-run beside_r96 "" ITR_VIT_RESERVE=96
-run beside_r96_f32 "" ITR_VIT_RESERVE=96 ITR_FWD_RESERVE=32
+run side ""
+run side_sync "" BENCH_STEP_TIMES=1
+run dflt "--stream default"
+run dflt_sync "--stream default" BENCH_STEP_TIMES=1
+run side20 "--steps 20"
+run old "--overlap 0" ITR_NO_WAVE=1
 cat gpurun_out/fvvar.log
