@@ -170,6 +170,15 @@ def pmc_traffic(n, mode, tag_hint=""):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))  # by round tag
     for f in reversed(files):
         d = json.load(open(f))
+        if mode == 3:  # Viterbi: the long-block sweep and the per-wave sweep of one call
+            parts = [(k, v) for k, v in d.items() if v.get("n_states", 70) == n and
+                     "hbm_bytes_raw" in v and ("wave_vit_kernel" in k or
+                                               (k.startswith("void itr::sweep_kernel<") and
+                                                k.endswith(", 3>(itr::SweepArgs)")))]
+            if len(parts) == 2:
+                return round(sum(v["hbm_bytes_raw"] for _, v in parts)), (
+                    f"{os.path.basename(f)} (" + " + ".join(k for k, _ in parts) +
+                    "): FETCH_SIZE+WRITE_SIZE per call, raw")
         for name, v in d.items():
             if name.startswith("void itr::sweep_kernel<") and \
                     name.endswith(f", {mode}>(itr::SweepArgs)") and \
@@ -396,9 +405,12 @@ def main():
             return
         if args.overlap and not timing:
             # forward + Viterbi in one call (itr_forward_viterbi): the forward sweep runs
-            # beside the Viterbi sweep's longest blocks on a disjoint set of CUs
+            # beside the Viterbi sweep's longest blocks on a disjoint set of CUs.  A step
+            # returns when its outputs are complete, like the reference's wrappers (measured:
+            # queueing the next step's fork/join behind the running one costs ~0.7 ms/step)
             hmm.forward_viterbi_device(model, plan, d_obs, out_ll=d_ll, out_path=d_path)
             exchange()
+            torch.cuda.current_stream().synchronize()
             return
         hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
         if timing:
@@ -480,8 +492,9 @@ def main():
         pair_ops = 2.0 * n * n  # per column: N^2 FMA (forward / backward) or N^2 add + N^2 max
         step_ms = dt / args.steps * 1e3
         if args.mode == "fv":
-            dom, dom_ms, dom_peak, dom_mode = "sweep_kernel<VIT> (Viterbi max-plus)", vit_avg, \
-                am_peak, 3
+            dom, dom_ms, dom_peak, dom_mode = ("Viterbi max-plus sweep: sweep_kernel<VIT> (longest "
+                                               "blocks, reserved CUs) | wave_vit_kernel (rest)"), \
+                vit_avg, am_peak, 3
             ideal_ms = pair_ops * cols_local / (fma_peak * 1e12) * 1e3 + \
                 pair_ops * cols_local / (am_peak * 1e12) * 1e3
         elif post_mode:

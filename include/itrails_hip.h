@@ -106,8 +106,9 @@ ITR_API int itr_forward_loglik(itr_model_t model, itr_plan_t plan, const uint16_
 ITR_API int itr_viterbi(itr_model_t model, itr_plan_t plan, const uint16_t* d_obs,
                         uint8_t* d_path, void* stream);
 
-/* itr_forward_loglik and itr_viterbi in one call (the same outputs, bit for bit), the
- * forward sweep overlapped with the Viterbi sweep's longest blocks on a disjoint set of CUs.
+/* itr_forward_loglik and itr_viterbi in one call (the same paths bit for bit; the same
+ * log-likelihoods to rounding: the forward may run in another layout), the forward sweep
+ * overlapped with the Viterbi sweep's longest blocks on a disjoint set of CUs.
  * For a caller that needs both over the same alignment (e.g. scoring a model and decoding
  * with it: loglik_wrapper then viterbi_wrapper, optimizer.py:40-65, 357-377). */
 ITR_API int itr_forward_viterbi(itr_model_t model, itr_plan_t plan, const uint16_t* d_obs,

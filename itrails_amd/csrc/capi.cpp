@@ -108,6 +108,9 @@ struct Partition {
   hipStream_t lng = nullptr, lng2 = nullptr;  // the reserved CUs
   hipStream_t blk = nullptr;                   // the other CUs
   hipEvent_t fork = nullptr, jl = nullptr, jl2 = nullptr, jb = nullptr;
+  hipStream_t blk2 = nullptr;  // experiment builds: a second stream on the other CUs
+  hipEvent_t jb2 = nullptr;
+  std::vector<uint32_t> mb;    // the other CUs' mask
 };
 thread_local std::deque<Partition> g_parts;
 
@@ -134,6 +137,7 @@ int partition(int reserve, Partition** out) {
   HIP_TRY(hipEventCreateWithFlags(&x.jl, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&x.jl2, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&x.jb, hipEventDisableTiming));
+  x.mb = mb;
   g_parts.push_back(x);
   *out = &g_parts.back();
   return 0;
@@ -162,6 +166,7 @@ struct itr_model {
   // log E with rows padded to the one-block-per-wave Viterbi layout's width (-inf columns),
   // when that layout serves this state count (wave_vit.hip)
   double* LEW = nullptr;
+  double* EW = nullptr;  // E likewise (zero columns) plus a row of ones (row 625)
   int xrw = 0;
 };
 
@@ -181,7 +186,7 @@ struct itr_plan {
   int32_t* d_order = nullptr;
   int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep,
                            // [3, 4] hybrid sweeps, [5, 6] Viterbi hybrid, [7] per-wave Viterbi,
-                           // [8, 9] the idle loop of a split hybrid launch
+                           // [8, 9] the idle loop of a split hybrid launch, [10] per-wave forward
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
   std::vector<int64_t> sorted_len;  // block lengths, longest first (processing order)
@@ -453,6 +458,16 @@ int itr_model_create(int n, const double* a, const double* la, const double* E,
     if (!e && hipMemcpy(m->LEW, lew.data(), lew.size() * sizeof(double),
                         hipMemcpyHostToDevice) != hipSuccess)
       e = fail(ITR_EHIP, "table upload failed");
+#ifdef ITR_EXPERIMENT  // the per-wave forward's table (experiment builds only)
+    std::vector<double> ew((size_t)(ITR_NOBS + 1) * w, 0.0);
+    for (int o = 0; o < ITR_NOBS; ++o)
+      for (int j = 0; j < n; ++j) ew[(size_t)o * w + j] = E[(size_t)o * n + j];
+    for (int j = 0; j < w; ++j) ew[(size_t)ITR_NOBS * w + j] = 1.0;
+    if (!e) e = dev_alloc(&m->EW, ew.size());
+    if (!e && hipMemcpy(m->EW, ew.data(), ew.size() * sizeof(double),
+                        hipMemcpyHostToDevice) != hipSuccess)
+      e = fail(ITR_EHIP, "table upload failed");
+#endif
     if (e) {
       itr_model_destroy(m);
       return e;
@@ -473,6 +488,7 @@ int itr_model_destroy(itr_model_t m) {
   dev_free(m->LPIE);
   dev_free(m->aT);
   dev_free(m->LEW);
+  dev_free(m->EW);
   delete m;
   return 0;
 }
@@ -854,8 +870,14 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     // with the forward sweep: its VALU tasks (the halves of the longest blocks, latency-bound)
     // beside the Viterbi long blocks on the reserved CUs, its matrix-core groups on the others
     const itr::MfmaGeometry gf = itr::mfma_geometry(m->n, itr::MODE_FWD_LL);
-    const bool split_fwd = fwd_loglik && nlong > 0 && gf.cfg >= 0 && p->ngroups_ll > 0 &&
-                           p->nutasks > 0 && p->nutasks < reserve_cus;
+    // (experiment builds: ITR_FV_WAVE_FWD=1 runs the forward in the per-wave layout on the
+    // other CUs before the per-wave Viterbi instead; measured slower, wave_vit.hip)
+    bool wave_fwd = false;
+#ifdef ITR_EXPERIMENT
+    wave_fwd = fwd_loglik && m->EW && p->ntasks > 0 && getenv("ITR_FV_WAVE_FWD");
+#endif
+    const bool split_fwd = fwd_loglik && !wave_fwd && nlong > 0 && gf.cfg >= 0 &&
+                           p->ngroups_ll > 0 && p->nutasks > 0 && p->nutasks < reserve_cus;
     itr::SweepArgs af = base_args(m, p, obs);
     af.mat = m->a;
     af.matT = m->aT;
@@ -890,19 +912,60 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       }
     }
     hipStream_t sb = pt ? pt->blk : st;
-    if (split_fwd) {
+    if (wave_fwd) {
+      itr::WaveFwdArgs f{};
+      f.n = m->n;
+      f.xr = wv.xr;
+      f.ntasks = p->ntasks;
+      f.tasks = p->d_tasks;
+      f.queue = p->d_queue + 10;
+      f.off = p->d_off;
+      f.obs = obs;
+      f.a = m->a;
+      f.aT = m->aT;
+      f.ew = m->EW;
+      f.emit = m->E;
+      f.init = m->PIE;
+      f.loglik = fwd_loglik;
+      f.svec = p->d_svec;
+      f.sK = p->d_sK;
+      f.prio_len = w.prio_len;
+      const int64_t grid = std::min<int64_t>(
+          (int64_t)wv.per_cu * (cus - (pt ? reserve_cus : 0)), (p->ntasks + 3) / 4);
+      HIP_TRY(hipMemsetAsync(f.queue, 0, sizeof(int), sb));
+      HIP_TRY(itr::launch_wave_fwd(wv, (int)grid, f, sb));
+    } else if (split_fwd) {
       if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, sb, nullptr, false, true,
                              (int64_t)gf.per_cu * (cus - reserve_cus), false))
         return e;
     } else if (fwd_loglik) {
       if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, sb)) return e;
     }
+    hipStream_t sw = sb;  // the per-wave sweep: after the forward's matrix-core groups
+    int wave_per_cu = wv.per_cu;
+#ifdef ITR_EXPERIMENT
+    // ... or beside them on a fourth stream (needs GPU_MAX_HW_QUEUES >= 5)
+    if (split_fwd && getenv("ITR_FV_BESIDE")) {
+      if (!pt->blk2) {
+        HIP_TRY(hipExtStreamCreateWithCUMask(&pt->blk2, (uint32_t)pt->mb.size() * 32,
+                                             pt->mb.data()));
+        HIP_TRY(hipEventCreateWithFlags(&pt->jb2, hipEventDisableTiming));
+      }
+      sw = pt->blk2;
+      HIP_TRY(hipStreamWaitEvent(sw, pt->fork, 0));
+      wave_per_cu = atoi(getenv("ITR_FV_BESIDE"));
+    }
+#endif
     if (w.nblocks > 0) {
       const int64_t work = (w.nblocks + 3) / 4;
       const int64_t grid =
-          std::min<int64_t>((int64_t)wv.per_cu * (cus - (pt ? reserve_cus : 0)), work);
-      HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), sb));
-      HIP_TRY(itr::launch_wave_vit(wv, (int)grid, w, sb));
+          std::min<int64_t>((int64_t)wave_per_cu * (cus - (pt ? reserve_cus : 0)), work);
+      HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), sw));
+      HIP_TRY(itr::launch_wave_vit(wv, (int)grid, w, sw));
+    }
+    if (sw != sb) {
+      HIP_TRY(hipEventRecord(pt->jb2, sw));
+      HIP_TRY(hipStreamWaitEvent(st, pt->jb2, 0));
     }
     if (pt) {
       HIP_TRY(hipEventRecord(pt->jl, pt->lng));
@@ -916,6 +979,9 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     }
     if (split_fwd)  // log P of the split blocks from their two halves
       HIP_TRY(itr::launch_fwd_split_combine(m->n, gf.xr, (int)p->nhsplit, p->d_hsplit_blk,
+                                            p->d_svec, p->d_sK, fwd_loglik, st));
+    if (wave_fwd)
+      HIP_TRY(itr::launch_fwd_split_combine(m->n, wv.xr, (int)p->nsplit, p->d_split_blk,
                                             p->d_svec, p->d_sK, fwd_loglik, st));
   } else if (vh.cfg >= 0) {
     // the longest blocks (longer than vfrac x the longest) as VALU tasks, the rest in
@@ -1183,9 +1249,9 @@ int itr_release_streams(void) {
   (void)hipGetDevice(&dev);
   for (auto& x : g_parts) {
     (void)hipSetDevice(x.device);
-    for (hipStream_t* q : {&x.lng, &x.lng2, &x.blk})
+    for (hipStream_t* q : {&x.lng, &x.lng2, &x.blk, &x.blk2})
       if (*q) (void)hipStreamDestroy(*q);
-    for (hipEvent_t* v : {&x.fork, &x.jl, &x.jl2, &x.jb})
+    for (hipEvent_t* v : {&x.fork, &x.jl, &x.jl2, &x.jb, &x.jb2})
       if (*v) (void)hipEventDestroy(*v);
   }
   g_parts.clear();

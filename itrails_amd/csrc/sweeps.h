@@ -157,7 +157,28 @@ struct WaveVitGeometry {
   size_t lds;   // dynamic LDS bytes
   int per_cu;   // resident workgroups per CU
 };
+// the forward log-likelihood sweep in the same layout (wave_vit.hip): the VALU sweep's tasks
+struct WaveFwdArgs {
+  int n;                        // hidden states
+  int xr;                       // stride of the split halves' vectors in svec
+  int64_t ntasks;
+  const int32_t* tasks;         // [ntasks x 3] {block, split, slot}, longest first (capi.cpp)
+  int* queue;                   // work counter, zero at launch
+  const int64_t* off;           // [plan blocks + 1]
+  const uint16_t* obs;          // [total]
+  const double* a;              // a, n x n
+  const double* aT;             // a^T (backward halves)
+  const double* ew;             // E, 626 x 8 iq: columns >= n zero, row 625 all ones
+  const double* emit;           // E, 625 x n (the backward half's first vector)
+  const double* init;           // pi E, 625 x n
+  double* loglik;               // [plan blocks]
+  double* svec;                 // [slots x 2 x xr]
+  int* sK;                      // [slots x 2]
+  int prio_len;                 // tasks at least this long run at raised wave priority
+};
 WaveVitGeometry wave_vit_geometry(int n);
+hipError_t launch_wave_fwd(const WaveVitGeometry& g, int grid, const WaveFwdArgs& p,
+                           hipStream_t st);
 hipError_t launch_wave_vit(const WaveVitGeometry& g, int grid, const VitArgs& p,
                            hipStream_t st);
 

@@ -211,6 +211,179 @@ __device__ __forceinline__ void wave_vit_blocks(const VitArgs& p, double* wl) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// EXPERIMENT (ITR_EXPERIMENT builds, ITR_FV_WAVE_FWD=1): the forward log-likelihood sweep (optimizer.py:165-188) in the same one-task-per-wavefront
+// layout: lane (g, q) holds the 9 x 9 slice of a (a^T for the backward half of a split
+// block), forms 9 partial sums over its sources by FMA, writes them to P, and finalises one
+// target (two for lanes 0-7) from the 8 partials: ~100 VALU instructions per column.  Tasks
+// are the VALU sweep's (capi.cpp itr_plan_create: whole blocks, and the two halves of the
+// blocks at least half as long as the longest: the forward over [0, m) and the textbook
+// backward over [m, Tb) with x'_t = beta_t e_t, whose last step multiplies by a row of ones),
+// the exact power-of-two rescale every 8 columns, the exponent kept as an integer, and the
+// same outputs (log P of whole blocks; the split halves' vectors and exponents for
+// fwd_split_combine).  Parity-green, but inside itr_forward_viterbi it made the step slower
+// than the matrix-core forward split over the two CU sets (10.2 vs 9.7 ms at chr10,
+// profiles/r2d_vit_layouts.txt): not adopted.
+#ifdef ITR_EXPERIMENT
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = fmax(v, __shfl_xor(v, d));
+  return v;
+}
+
+template <int IQ>
+__device__ __forceinline__ void wave_fwd_tasks(const WaveFwdArgs& p, double* wl) {
+  using C = WaveVit<IQ>;
+  constexpr int XRW = C::XRW, NB = C::NB, IQS = C::IQS, XN = C::XN, PS = C::PS, HT = C::HT,
+                NI = C::NI, EB = C::EB;
+  const int l = threadIdx.x & 63, q = l & 7, g = l >> 3;
+  const int n = p.n;
+  double* X = wl;
+  double* P = X + C::LX;
+  double* EST = P + C::LP;
+  uint16_t* SYM = reinterpret_cast<uint16_t*>(EST + C::LE);
+  const int A = l, B = 64 + (l & 7);
+  const bool inA = A < XRW && A < n;
+  const bool inB = NB > 0 && B < n;
+  const bool ownB = inB && l < NB;
+  const int sA = A < XRW ? (A / IQ) * IQS + A % IQ : XN + l;
+  const int sB = (NB > 0 && l < NB) ? (B / IQ) * IQS + B % IQ : XN + l;
+  const int rA = A < XRW ? A : 0, rB = NB > 0 ? B : 0;
+  for (int i = l; i < C::LX; i += 64) X[i] = 0.0;  // pad sources contribute nothing
+
+  for (;;) {
+    const int bi = uni(atomicAdd(p.queue, l == 0 ? 1 : 0));  // see wave_vit_blocks
+    if (bi >= p.ntasks) break;
+    const int32_t* td = p.tasks + 3 * bi;
+    const int blk = uni(td[0]), split = uni(td[1]), slot = uni(td[2]);
+    const int64_t c0 = p.off[blk];
+    const int Tb = uni((int)(p.off[blk + 1] - c0));
+    const int T = split > 0 ? split : (split < 0 ? Tb + split + 1 : Tb);
+    if (T <= 0) {
+      if (split == 0 && l == 0) p.loglik[blk] = 0.0;  // log-likelihood of nothing
+    } else {
+      const int dir = split < 0 ? -1 : 1;
+      // the slice of a (a^T for a backward half), loaded per task: a few L2 loads against
+      // thousands of steps
+      double m[IQ][IQ];
+      {
+        const double* M = dir > 0 ? p.a : p.aT;
+#pragma unroll
+        for (int k = 0; k < IQ; ++k)
+#pragma unroll
+          for (int r = 0; r < IQ; ++r) {
+            const int i = IQ * q + k, j = IQ * g + r;
+            m[k][r] = (i < n && j < n) ? M[(int64_t)i * n + j] : 0.0;
+          }
+      }
+      const bool urgent = T >= p.prio_len;
+      if (urgent) __builtin_amdgcn_s_setprio(3);
+      const uint16_t* ob = p.obs + c0;
+      auto symg = [&](int s) -> int {
+        const int s1 = min(s, Tb - 1);
+        return min((int)ob[dir > 0 ? s1 : Tb - 1 - s1], 624);
+      };
+      SYM[l] = (uint16_t)symg(l);
+      SYM[64 + l] = (uint16_t)symg(64 + l);
+      int sin = symg(128 + l);
+      // emission row of step s: the column's symbol; the backward half's last step: the row of
+      // ones (row 625 of the padded table)
+      auto srow = [&](int s) -> int {
+        return (split < 0 && s == T - 1) ? 625 : (int)SYM[((s >> 6) & 1) * 64 + (s & 63)];
+      };
+      auto stage_issue = [&](int h) {
+        double* d = EST + (h & 1) * EB;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const int e = 128 * i + 2 * l;
+          const double* src = p.ew;
+          if (e < HT * XRW) src += (int64_t)srow(h * HT + e / XRW) * XRW + e % XRW;
+          __builtin_amdgcn_global_load_lds(
+              src, (__attribute__((address_space(3))) void*)(d + 128 * i), 16, 0, 0);
+        }
+      };
+      auto stage_wait = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+      const int o0 = (int)SYM[0];
+      const double* x0tab = dir < 0 ? p.emit : p.init;  // x'_{Tb-1} = e_{Tb-1}; alpha_0 = pi e_0
+      double xA = inA ? x0tab[o0 * n + A] : 0.0;
+      double xB = inB ? x0tab[o0 * n + B] : 0.0;
+      X[sA] = xA;
+      X[sB] = xB;
+      int K = 0;  // sum of the power-of-two exponents divided out
+      stage_issue(0);
+      stage_wait();
+      stage_issue(1);
+      for (int t0 = 0; t0 < T; t0 += 16) {
+#pragma unroll
+        for (int sub = 0; sub < 16; ++sub) {
+          const int t = t0 + sub;
+          if (t >= 1 && t < T) {
+            if ((sub & (HT - 1)) == 0) {  // half-tile boundary (t >= 8)
+              stage_wait();
+              if ((t & 63) == 0) {
+                SYM[(((t >> 6) + 1) & 1) * 64 + l] = (uint16_t)sin;
+                sin = symg(t + 128 + l);
+              }
+              stage_issue(t / HT + 1);
+            }
+            const double* es = EST + ((t / HT) & 1) * EB + (t & (HT - 1)) * XRW;
+            double ecA = es[rA];
+            double ecB = es[rB];
+            if ((sub & 7) == 1) {  // exact 2^-e rescale by the max of x_{t-1}, into the factors
+              const double Mx = wave_max(fmax(inA ? xA : 0.0, ownB ? xB : 0.0));
+              const int e = (Mx > 0.0 && Mx < INFINITY) ? ilogb(Mx) : 0;
+              const double sc = ldexp(1.0, -e);
+              K += e;
+              ecA *= sc;
+              ecB *= sc;
+            }
+            double xs[IQ];
+#pragma unroll
+            for (int k = 0; k < IQ; ++k) xs[k] = X[q * IQS + k];
+            double z[IQ];
+#pragma unroll
+            for (int r = 0; r < IQ; ++r) z[r] = xs[0] * m[0][r];
+#pragma unroll
+            for (int k = 1; k < IQ; ++k)
+#pragma unroll
+              for (int r = 0; r < IQ; ++r) z[r] = fma(xs[k], m[k][r], z[r]);
+#pragma unroll
+            for (int r = 0; r < IQ; ++r) P[(IQ * g + r) * PS + q] = z[r];
+            const double* pa = P + rA * PS;
+            xA = (((pa[0] + pa[1]) + (pa[2] + pa[3])) + ((pa[4] + pa[5]) + (pa[6] + pa[7]))) * ecA;
+            if constexpr (NB > 0) {
+              const double* pb = P + rB * PS;
+              xB = (((pb[0] + pb[1]) + (pb[2] + pb[3])) + ((pb[4] + pb[5]) + (pb[6] + pb[7]))) *
+                   ecB;
+            }
+            X[sA] = xA;
+            X[sB] = xB;
+          }
+        }
+      }
+      if (split != 0) {  // half of a split block: the scaled vector and its exponent
+        const int side = split < 0;
+        double* sv = p.svec + ((int64_t)slot * 2 + side) * p.xr;
+        if (inA) sv[A] = xA;
+        if (ownB) sv[B] = xB;
+        if (l == 0) p.sK[slot * 2 + side] = K;
+      } else {  // log P = log(sum_j x_j) + K ln 2   (optimizer.py:160-162)
+        const double tot = wave_sum((inA ? xA : 0.0) + (ownB ? xB : 0.0));
+        if (l == 0) p.loglik[blk] = log(tot) + (double)K * LN2;
+      }
+      if (urgent) __builtin_amdgcn_s_setprio(0);
+    }
+  }
+}
+
+template <int IQ>
+__global__ void __launch_bounds__(64 * kWaves, 2) wave_fwd_kernel(WaveFwdArgs p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  wave_fwd_tasks<IQ>(p, reinterpret_cast<double*>(smem) +
+                            (size_t)(threadIdx.x >> 6) * WaveVit<IQ>::WL);
+}
+#endif  // ITR_EXPERIMENT
+
 template <int IQ>
 __global__ void __launch_bounds__(64 * kWaves, 2) wave_vit_kernel(VitArgs p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -235,6 +408,22 @@ WaveVitGeometry wave_vit_geometry(int n) {
     nb = 1;
   g.per_cu = nb;
   return g;
+}
+
+hipError_t launch_wave_fwd(const WaveVitGeometry& g, int grid, const WaveFwdArgs& p,
+                           hipStream_t st) {
+#ifndef ITR_EXPERIMENT
+  (void)g, (void)grid, (void)p, (void)st;
+  return hipErrorInvalidValue;
+#else
+  switch (g.iq) {
+    case 9:
+      hipLaunchKernelGGL(wave_fwd_kernel<9>, dim3(grid), dim3(g.block), g.lds, st, p);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+#endif
 }
 
 hipError_t launch_wave_vit(const WaveVitGeometry& g, int grid, const VitArgs& p,

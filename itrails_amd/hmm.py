@@ -180,8 +180,9 @@ def viterbi_device(model: Model, plan: Plan, d_obs, out=None):
 
 
 def forward_viterbi_device(model: Model, plan: Plan, d_obs, out_ll=None, out_path=None):
-    """forward_loglik_device and viterbi_device in one call (identical outputs), the forward
-    sweep overlapped with the Viterbi sweep's longest blocks (itr_forward_viterbi)."""
+    """forward_loglik_device and viterbi_device in one call (identical paths, log-likelihoods
+    equal to rounding), the forward sweep overlapped with the Viterbi sweep's longest blocks
+    (itr_forward_viterbi)."""
     import torch
 
     _check_obs(plan, d_obs)

@@ -6,4 +6,4 @@ d = json.load(open(sys.argv[1]))
 r = d["roofline"]
 print(" ".join(sys.argv[2:]), round(d["value"] / 1e6, 1), "Mcol/s fwd", r.get("forward_ms"),
       "vit", r.get("kernel_ms"), "trace", r.get("traceback_ms"), "fv", r.get("forward_viterbi_ms"),
-      "ms/step", d.get("ms_per_step"), "check", d.get("check"))
+      "ms/step", d.get("ms_per_step"), "vit_eq", d.get("viterbi_equal"), "ll_err", d.get("loglik_max_rel_err"))

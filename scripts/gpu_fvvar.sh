@@ -11,7 +11,8 @@ run() {  # label, bench args, then env assignments
 run side ""
 run side_sync "" BENCH_STEP_TIMES=1
 run dflt "--stream default"
-run dflt_sync "--stream default" BENCH_STEP_TIMES=1
-run side20 "--steps 20"
+run side_q8 "" GPU_MAX_HW_QUEUES=8
+run q8_beside1 "" GPU_MAX_HW_QUEUES=8 ITR_FV_BESIDE=1
+run q8_beside2 "" GPU_MAX_HW_QUEUES=8 ITR_FV_BESIDE=2
 run old "--overlap 0" ITR_NO_WAVE=1
 cat gpurun_out/fvvar.log

@@ -6,18 +6,14 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_sweeps.py tests/test_gpu_fu
 tail -2 gpurun_out/pytest_wave.log
 run() {  # label, bench args, then env assignments
   label=$1; bargs=$2; shift 2
-  env ITR_LIB=itrails_amd/libitrails_hip_exp.so "$@" timeout -k 10 120 python bench.py --steps 5 --warmup 2 --verify 0 --cpu-1core-cols 0 --host-path 0 $bargs > gpurun_out/ws.json 2>> gpurun_out/ws.err || { echo "FAIL $label" >> gpurun_out/wavesweep.log; cat gpurun_out/wavesweep.log; exit 1; }
+  env ITR_LIB=itrails_amd/libitrails_hip_exp.so "$@" timeout -k 10 120 python bench.py --steps 5 --warmup 2 --verify 1 --cpu-1core-cols 0 --host-path 0 $bargs > gpurun_out/ws.json 2>> gpurun_out/ws.err || { echo "FAIL $label" >> gpurun_out/wavesweep.log; cat gpurun_out/wavesweep.log; exit 1; }
   python scripts/bench_line.py gpurun_out/ws.json "$label" >> gpurun_out/wavesweep.log
 }
 run old "--overlap 0" ITR_NO_WAVE=1
-run def ""
-run def_noov "--overlap 0"
-run f8 "" ITR_FWD_RESERVE=8
-run f16 "" ITR_FWD_RESERVE=16
-run r80 "" ITR_VIT_RESERVE=80
-run r96 "" ITR_VIT_RESERVE=96
-run r80_l35 "" ITR_VIT_RESERVE=80 ITR_VIT_LONG_FRAC=0.35
-run r64_l40 "" ITR_VIT_LONG_FRAC=0.40
-run lb_def "--block-len 100000"
-run short_def "--mean-block 300"
+run wfwd ""
+run wfwd_r48 "" ITR_VIT_RESERVE=48
+run wfwd_r80 "" ITR_VIT_RESERVE=80
+run hyb "" ITR_FV_HYBRID=1
+run lb "--block-len 100000"
+run short "--mean-block 300"
 cat gpurun_out/wavesweep.log

@@ -160,8 +160,9 @@ def test_viterbi_frequent_switches(gpu, n):
 @pytest.mark.parametrize("n", [46, 65, 70, 72])
 def test_forward_viterbi_call_matches_separate_calls(gpu, n):
     """itr_forward_viterbi (forward sweep beside the Viterbi sweep's longest blocks on a
-    disjoint CU set) returns exactly what itr_forward_loglik and itr_viterbi return, and the
-    Viterbi path is the oracle's.  Blocks of 2,048+ columns go to the long-block launch."""
+    disjoint CU set) returns what itr_forward_loglik and itr_viterbi return (paths bit for
+    bit, log-likelihoods to 1e-12), and both match the oracle.  Blocks of 2,048+ columns go to
+    the long-block launch; blocks of half the longest or more are split forward tasks."""
     import torch
 
     rng = np.random.default_rng(70 + n)
@@ -175,7 +176,9 @@ def test_forward_viterbi_call_matches_separate_calls(gpu, n):
     p1 = hmm.viterbi_device(model, plan, d_obs).cpu().numpy()
     ll2, p2 = hmm.forward_viterbi_device(model, plan, d_obs)
     ll2, p2 = ll2.cpu().numpy(), p2.cpu().numpy()
-    np.testing.assert_array_equal(ll2, ll1)
+    # the combined call's forward may use another layout (per-wave FMA chains): the same
+    # log-likelihoods to rounding, the same paths bit for bit
+    np.testing.assert_allclose(ll2, ll1, rtol=1e-12, atol=0)
     np.testing.assert_array_equal(p2, p1)
     np.testing.assert_array_equal(p2, O.viterbi(t, obs, off))
     np.testing.assert_allclose(ll2, O.forward_loglik(t, obs, off), rtol=RTOL, atol=0)
