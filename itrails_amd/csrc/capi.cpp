@@ -890,7 +890,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     af.sK = p->d_sK;
     int64_t rf = 0;  // reserved CUs for the forward's VALU tasks
     if (split_fwd) {
-      rf = std::min<int64_t>(p->nutasks, reserve_cus / 4);
+      rf = std::min<int64_t>(p->nutasks, 3 * reserve_cus / 8);
 #ifdef ITR_EXPERIMENT
       if (getenv("ITR_FWD_RESERVE")) rf = std::min<int64_t>(atoi(getenv("ITR_FWD_RESERVE")), reserve_cus - 1);
 #endif

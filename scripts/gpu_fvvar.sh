@@ -8,11 +8,11 @@ run() {  # label, bench args, then env assignments
   python scripts/bench_line.py gpurun_out/ws.json "$label" >> gpurun_out/fvvar.log
   grep "^step" gpurun_out/ws.err | tr '\n' ' ' >> gpurun_out/fvvar.log; echo >> gpurun_out/fvvar.log
 }
-run side ""
-run side_sync "" BENCH_STEP_TIMES=1
-run dflt "--stream default"
-run side_q8 "" GPU_MAX_HW_QUEUES=8
-run q8_beside1 "" GPU_MAX_HW_QUEUES=8 ITR_FV_BESIDE=1
-run q8_beside2 "" GPU_MAX_HW_QUEUES=8 ITR_FV_BESIDE=2
-run old "--overlap 0" ITR_NO_WAVE=1
+run def ""
+run r72_l40_f16 "" ITR_VIT_RESERVE=72 ITR_VIT_LONG_FRAC=0.40 ITR_FWD_RESERVE=16
+run r80_l40_f20 "" ITR_VIT_RESERVE=80 ITR_VIT_LONG_FRAC=0.40 ITR_FWD_RESERVE=20
+run r96_l35_f24 "" ITR_VIT_RESERVE=96 ITR_VIT_LONG_FRAC=0.35 ITR_FWD_RESERVE=24
+run r64_f24 "" ITR_FWD_RESERVE=24
+run r56_l50_f14 "" ITR_VIT_RESERVE=56 ITR_VIT_LONG_FRAC=0.50 ITR_FWD_RESERVE=14
+run r64_l50_f20 "" ITR_VIT_LONG_FRAC=0.50 ITR_FWD_RESERVE=20
 cat gpurun_out/fvvar.log
