@@ -876,8 +876,13 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
 #ifdef ITR_EXPERIMENT
     wave_fwd = fwd_loglik && m->EW && p->ntasks > 0 && getenv("ITR_FV_WAVE_FWD");
 #endif
+    // (the VALU halves must not outnumber the reserved CUs; experiment builds: ITR_FV_SPLIT_CAP)
+    int64_t split_cap = reserve_cus;
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_FV_SPLIT_CAP")) split_cap = atoi(getenv("ITR_FV_SPLIT_CAP"));
+#endif
     const bool split_fwd = fwd_loglik && !wave_fwd && nlong > 0 && gf.cfg >= 0 &&
-                           p->ngroups_ll > 0 && p->nutasks > 0 && p->nutasks < reserve_cus;
+                           p->ngroups_ll > 0 && p->nutasks > 0 && p->nutasks < split_cap;
     itr::SweepArgs af = base_args(m, p, obs);
     af.mat = m->a;
     af.matT = m->aT;
