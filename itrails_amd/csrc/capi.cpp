@@ -821,9 +821,9 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   // The longest blocks (longer than lfrac x the longest, at least 2,048 columns) on the
   // 9-wave VALU layout on `reserve_cus` reserved CUs; the rest one block per wavefront on the
   // other CUs (a lone wave steps ~2x slower, so the per-wave sweep must not get blocks
-  // longer than ~half the longest).  When the long blocks do not fit the reserved CUs within
-  // the longest block's time (workloads of few, equally long blocks), every block goes to
-  // the 9-wave layout on all CUs.
+  // longer than ~half the longest).  When the long blocks would keep the reserved CUs busy
+  // longer than the rest keeps the others (workloads of few, equally long blocks), every
+  // block goes to the 9-wave layout on all CUs.
   const int cus = cu_count();
   int reserve_cus = cus / 4;
   double lfrac = 0.45;
@@ -841,7 +841,13 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       cum += p->sorted_len[nlong];
       ++nlong;
     }
-    if (cum > (int64_t)reserve_cus * tmax) wave = false;
+    // Keep the partition when the reserved CUs finish the long blocks no later than the other
+    // CUs finish the rest (or than the longest block alone).  Measured at N = 70: ~325 ns per
+    // column for a block alone on its CU in the 9-wave layout; ~114 CU-ns per column for the
+    // per-wave sweep on a loaded CU (5.3 ms for 8.9 M columns on 192 CUs).
+    const double t_long = (double)cum * 325e-9 / reserve_cus;
+    const double t_bulk = (double)(p->total - cum) * 114e-9 / (cus - reserve_cus);
+    if (t_long > 1.1 * std::max(t_bulk, (double)tmax * 325e-9)) wave = false;
   }
   if (!wave && fwd_loglik)  // no overlap: the forward sweep first, on the caller's stream
     if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, st)) return e;
