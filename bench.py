@@ -299,6 +299,11 @@ def main():
                          "rehearse the exchange with several ranks on one GPU)")
     args = ap.parse_args()
 
+    if args.gpus > 1:
+        # RCCL's own streams beside the launch stream and the three CU-masked streams of
+        # itr_forward_viterbi exceed the 4 hardware queues a process gets by default; shared
+        # queues serialise.  Set before HIP starts (ranks inherit it).
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
 
