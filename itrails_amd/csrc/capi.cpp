@@ -845,9 +845,11 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     // CUs finish the rest (or than the longest block alone).  Measured at N = 70: ~325 ns per
     // column for a block alone on its CU in the 9-wave layout; ~114 CU-ns per column for the
     // per-wave sweep on a loaded CU (5.3 ms for 8.9 M columns on 192 CUs).
-    const double t_long = (double)cum * 325e-9 / reserve_cus;
-    const double t_bulk = (double)(p->total - cum) * 114e-9 / (cus - reserve_cus);
-    if (t_long > 1.1 * std::max(t_bulk, (double)tmax * 325e-9)) wave = false;
+    auto t_long = [&](int64_t c) { return (double)c * 325e-9 / reserve_cus; };
+    auto t_bulk = [&](int64_t c) { return (double)(p->total - c) * 114e-9 / (cus - reserve_cus); };
+    // (moving more long blocks to the reserved CUs until both sides balance by this estimate
+    // was measured slower: chr10 Viterbi 5.65 -> 6.43 ms, chr100 47.6 -> 50.6 ms)
+    if (t_long(cum) > 1.1 * std::max(t_bulk(cum), (double)tmax * 325e-9)) wave = false;
   }
   if (!wave && fwd_loglik)  // no overlap: the forward sweep first, on the caller's stream
     if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, st)) return e;
