@@ -83,6 +83,15 @@ ITR_API int itr_model_n_states(itr_model_t model, int* n);
 /* device workspace (Viterbi back-pointers, forward rows for posteriors).              */
 /* ---------------------------------------------------------------------------------- */
 ITR_API int itr_plan_create(const int64_t* h_block_off, int64_t n_blocks, itr_plan_t* out);
+/* itr_plan_create with the work-decomposition knobs explicit (negative = default):
+ *   split_frac       forward log-likelihood: blocks at least this share of the longest (and
+ *                    >= 512 columns) run as two halves joined exactly (default 0.5; 0 = off)
+ *   post_split_frac  posterior on few long blocks: blocks at least this share of the longest
+ *                    get their backward sweep beside the forward one (default 0.25; 0 = off)
+ * Results agree with the unsplit sweeps to rounding (log-likelihoods, posteriors) or bit for
+ * bit (Viterbi paths). */
+ITR_API int itr_plan_create_ex(const int64_t* h_block_off, int64_t n_blocks, double split_frac,
+                               double post_split_frac, itr_plan_t* out);
 ITR_API int itr_plan_destroy(itr_plan_t plan);
 ITR_API int itr_plan_total_columns(itr_plan_t plan, int64_t* total);
 /* grow the workspace now (optional; the sweeps grow it on demand) */
@@ -139,7 +148,10 @@ ITR_API int itr_posterior_host(itr_model_t model, itr_plan_t plan, const uint16_
                                double* h_post);
 /* itr_posterior_host keeps two 128 MB pinned staging buffers (plus a stream and two events)
  * per calling thread for large copy-outs, bound to the thread's current device and
- * recreated when it changes; this frees the calling thread's set. */
+ * recreated when it changes; itr_vanloan_paths keeps a grow-only device workspace and a
+ * pinned staging buffer per calling thread and device.  This frees the calling thread's
+ * sets (after the thread's last Van Loan evaluation has finished on the device); another
+ * thread's sets are untouched and are freed when that thread exits. */
 ITR_API int itr_release_staging(void);
 /* itr_viterbi / itr_forward_viterbi keep three CU-masked streams (and four events) per
  * calling thread and device; this destroys the calling thread's set. */

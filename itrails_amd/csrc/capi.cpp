@@ -112,12 +112,31 @@ struct Partition {
   hipEvent_t jb2 = nullptr;
   std::vector<uint32_t> mb;    // the other CUs' mask
 };
-thread_local std::deque<Partition> g_parts;
+// The calling thread's partitions; destroyed with the thread (each thread that decodes owns
+// its streams, so a worker thread's exit returns its hardware-queue streams)
+struct Partitions {
+  std::deque<Partition> v;
+  void release() {
+    int dev = 0;
+    const bool have_dev = hipGetDevice(&dev) == hipSuccess;
+    for (auto& x : v) {
+      (void)hipSetDevice(x.device);
+      for (hipStream_t* q : {&x.lng, &x.lng2, &x.blk, &x.blk2})
+        if (*q) (void)hipStreamDestroy(*q);
+      for (hipEvent_t* e : {&x.fork, &x.jl, &x.jl2, &x.jb, &x.jb2})
+        if (*e) (void)hipEventDestroy(*e);
+    }
+    v.clear();
+    if (have_dev) (void)hipSetDevice(dev);
+  }
+  ~Partitions() { release(); }
+};
+thread_local Partitions g_parts;
 
 int partition(int reserve, Partition** out) {
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
-  for (auto& x : g_parts)
+  for (auto& x : g_parts.v)
     if (x.device == dev && x.reserve == reserve) {
       *out = &x;
       return 0;
@@ -138,8 +157,8 @@ int partition(int reserve, Partition** out) {
   HIP_TRY(hipEventCreateWithFlags(&x.jl2, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&x.jb, hipEventDisableTiming));
   x.mb = mb;
-  g_parts.push_back(x);
-  *out = &g_parts.back();
+  g_parts.v.push_back(x);
+  *out = &g_parts.v.back();
   return 0;
 }
 
@@ -244,6 +263,16 @@ int vit_stride(int n) {  // record stride of the Viterbi workspace for this stat
   return vh.cfg >= 0 ? vh.xr : itr::sweep_row_stride(n, itr::MODE_VIT);
 }
 
+// The posterior's concurrent split (launch_post_split): only on the VALU-only posterior
+// (no matrix-core form at this state count) and only where the blocks are few
+// (latency-bound: 10 Mbp in 100 blocks of 100 kbp, 96.9 -> 60 ms); with thousands of blocks
+// the sweeps are throughput-bound and the extra beta rows cost more than the shorter tail
+// (chr10: 20.7 vs 23.4 ms).  reserve() sizes the beta rows by the same test.
+bool post_split_path(int n, itr_plan_t p) {
+  return p->npsplit > 0 && n <= 128 && p->nblocks <= 2 * (int64_t)cu_count() &&
+         itr::mfma_geometry(n, itr::MODE_FWD_STORE).cfg < 0;
+}
+
 int reserve(itr_plan_t p, int n, bool vit, bool post) {
   const int xr = vit_stride(n);
   const int xa = itr::sweep_row_stride(n, itr::MODE_BWD);
@@ -263,7 +292,7 @@ int reserve(itr_plan_t p, int n, bool vit, bool post) {
     const int stride = g.cfg >= 0 ? std::max(xa, g.xr) : xa;
     need_rows = std::max(need_rows, (size_t)p->total * stride);
   }
-  if (post && p->beta_rows > 0 && (size_t)p->beta_rows * xa > p->beta_cap) {
+  if (post && post_split_path(n, p) && (size_t)p->beta_rows * xa > p->beta_cap) {
     dev_free(p->d_beta);
     if (int e = dev_alloc(&p->d_beta, (size_t)p->beta_rows * xa)) return e;
     p->beta_cap = (size_t)p->beta_rows * xa;
@@ -500,6 +529,11 @@ int itr_model_n_states(itr_model_t m, int* n) {
 }
 
 int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
+  return itr_plan_create_ex(off, nblocks, -1.0, -1.0, out);
+}
+
+int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
+                       double post_split_frac, itr_plan_t* out) {
   if (!out) return fail(ITR_EINVAL, "null output pointer");
   *out = nullptr;
   if (nblocks < 0 || (nblocks > 0 && !off)) return fail(ITR_EINVAL, "bad block offsets");
@@ -541,10 +575,9 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   //   the hybrid sweeps' own lists below.
   const int64_t tmax = nblocks ? h_off[order[0] + 1] - h_off[order[0]] : 0;
   std::vector<int32_t> split_blk;
-  // ITR_SPLIT_FRAC (read once here, at plan creation): 0 disables the split (tests compare
-  // the split forward with the unsplit one)
-  const char* fr = getenv("ITR_SPLIT_FRAC");
-  const double frac = fr ? atof(fr) : 0.5;
+  // split_frac (itr_plan_create_ex; negative = the default 0.5): 0 disables the split (tests
+  // compare the split forward with the unsplit one)
+  const double frac = split_frac < 0 ? 0.5 : split_frac;
   auto is_split = [&](int64_t T) {
     return frac > 0 && T >= 512 && (double)T >= frac * (double)tmax;
   };
@@ -556,12 +589,11 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
       split_blk.push_back(b);
     }
   }
-  // posterior split set (blocks at least a quarter as long as the longest, >= 512 columns;
-  // ITR_POST_SPLIT_FRAC read once here, 0 disables): a prefix of the order
+  // posterior split set (blocks at least post_split_frac of the longest, default a quarter,
+  // >= 512 columns; 0 disables): a prefix of the order
   std::vector<int64_t> boff(nblocks, -1);
   {
-    const char* pf = getenv("ITR_POST_SPLIT_FRAC");
-    const double pfrac = pf ? atof(pf) : 0.25;
+    const double pfrac = post_split_frac < 0 ? 0.25 : post_split_frac;
     int64_t rows = 0, k = 0;
     for (; k < nblocks; ++k) {
       const int64_t T = h_off[order[k] + 1] - h_off[order[k]];
@@ -1093,10 +1125,7 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
     return run_hybrid(itr::MODE_BWD, m, p, a, gb, st, "posterior_bwd");
   }
   const int nl = (int)p->npsplit;
-  // only where the blocks are few (latency-bound: 10 Mbp in 100 blocks of 100 kbp, 96.9 ->
-  // 60 ms); with thousands of blocks the sweeps are throughput-bound and the extra beta
-  // rows cost more than the shorter tail (chr10: 20.7 vs 23.4 ms)
-  if (nl > 0 && m->n <= 128 && p->nblocks <= 2 * (int64_t)cu_count()) {
+  if (post_split_path(m->n, p)) {
     // the longest blocks: backward sweep (beta rows) concurrently with every block's forward
     // sweep; then the short blocks' backward+posterior sweep and the long blocks' combine
     itr::SweepGeometry g = itr::sweep_geometry(m->n, itr::MODE_BWD);
@@ -1258,17 +1287,7 @@ int itr_posterior_host(itr_model_t m, itr_plan_t p, const uint16_t* h_obs, doubl
 }
 
 int itr_release_streams(void) {
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  for (auto& x : g_parts) {
-    (void)hipSetDevice(x.device);
-    for (hipStream_t* q : {&x.lng, &x.lng2, &x.blk, &x.blk2})
-      if (*q) (void)hipStreamDestroy(*q);
-    for (hipEvent_t* v : {&x.fork, &x.jl, &x.jl2, &x.jb, &x.jb2})
-      if (*v) (void)hipEventDestroy(*v);
-  }
-  g_parts.clear();
-  (void)hipSetDevice(dev);
+  g_parts.release();
   return 0;
 }
 

@@ -68,13 +68,6 @@ __global__ void __launch_bounds__(64 * WV, (Occ<QL, WV, RJN, IQ, MODE>::value))
 // max(yd, yo) because IEEE rounding is monotone — and kept for further switches in the
 // same tile.
 // ---------------------------------------------------------------------------------------
-// LDS hand-off between lanes of one wave (the region is private to the wave)
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-}
-
 template <int G>  // state groups of 64 lanes: n <= 64 G
 __global__ void __launch_bounds__(256) vit_trace_kernel(TraceArgs p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

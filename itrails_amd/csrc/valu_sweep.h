@@ -125,6 +125,15 @@ __device__ __forceinline__ double row_sum(double v) {
   return v + dpp_f64<DPP_R8>(v);
 }
 
+// LDS hand-off between lanes of one wave (the region is private to the wave): a wave's LDS
+// instructions execute in order, so this costs no instruction; it keeps the compiler from
+// moving the reads above the writes or forwarding values around them
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
 // s_waitcnt vmcnt(0) (expcnt/lgkmcnt untouched).  Issued once before each step loop so
 // that no loop-carried register is the destination of a load in flight at loop entry:
 // otherwise hipcc's waitcnt pass puts a vmcnt(0) INSIDE the loop at that register's first

@@ -267,7 +267,9 @@ void branch_of(double norm, int* m, int* s) {  // expm.py:26-143
   }
 }
 
-// grow-only device workspace and pinned staging, per device
+// grow-only device workspace and pinned staging, per device and calling thread (two threads
+// evaluating on one device must not share the staging buffer or the workspace); a call
+// waits for the previous call of its thread on that device (`done`) before reusing them
 struct Ws {
   int dev = -1;
   char* d = nullptr;
@@ -276,13 +278,26 @@ struct Ws {
   size_t hbytes = 0;
   hipEvent_t done = nullptr;
 };
-Ws g_ws[16];
+struct WsSet {
+  Ws w[16];
+  void release() {
+    for (Ws& x : w) {
+      if (x.done) (void)hipEventSynchronize(x.done);  // the last call's kernels are done
+      if (x.d) (void)hipFree(x.d);
+      if (x.h) (void)hipHostFree(x.h);
+      if (x.done) (void)hipEventDestroy(x.done);
+      x = Ws{};
+    }
+  }
+  ~WsSet() { release(); }
+};
+thread_local WsSet g_ws;
 
 hipError_t ws_get(size_t dbytes, size_t hbytes, Ws** out) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e) return e;
-  Ws& w = g_ws[dev & 15];
+  Ws& w = g_ws.w[dev & 15];
   if (!w.done) {
     if ((e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming))) return e;
   } else if ((e = hipEventSynchronize(w.done))) {  // the previous call has finished
@@ -310,14 +325,7 @@ hipError_t ws_get(size_t dbytes, size_t hbytes, Ws** out) {
 
 }  // namespace
 
-void release_vanloan_workspace() {
-  for (Ws& w : g_ws) {
-    if (w.d) (void)hipFree(w.d);
-    if (w.h) (void)hipHostFree(w.h);
-    if (w.done) (void)hipEventDestroy(w.done);
-    w = Ws{};
-  }
-}
+void release_vanloan_workspace() { g_ws.release(); }
 
 hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t, int nmasks,
                          const uint8_t* h_masks, int64_t npaths, const int32_t* h_job,

@@ -169,6 +169,7 @@ __device__ __forceinline__ void wave_vit_blocks(const VitArgs& p, double* wl) {
               for (int r = 0; r < IQ; ++r) z[r] = fmax(z[r], xs[k] + m[k][r]);
 #pragma unroll
             for (int r = 0; r < IQ; ++r) P[(IQ * g + r) * PS + q] = z[r];
+            wave_lds_sync();  // partials of the other lanes visible
             // this lane's target(s): max over the 8 source chunks (exact, order-free)
             const double* pa = P + rA * PS;
             const double zoA = fmax(fmax(fmax(pa[0], pa[1]), fmax(pa[2], pa[3])),
@@ -188,6 +189,7 @@ __device__ __forceinline__ void wave_vit_blocks(const VitArgs& p, double* wl) {
             }
             X[sA] = xA;
             X[sB] = xB;
+            wave_lds_sync();  // omega_t visible to every lane for the next step
             if (sub == 0) {  // the tile's checkpoint row (t = t0 >= 16)
               if (inA) p.ckpt[rec + A] = xA;
               if (ownB) p.ckpt[rec + B] = xB;

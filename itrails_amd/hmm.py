@@ -93,9 +93,12 @@ def concat_blocks(V_lst: Sequence[np.ndarray]):
 
 
 class Plan:
-    """Block layout of one alignment on the current device (itr_plan_create)."""
+    """Block layout of one alignment on the current device (itr_plan_create_ex).
 
-    def __init__(self, block_off):
+    split_frac / post_split_frac: the plan's work-decomposition knobs (None = the library's
+    defaults; 0 disables the split forward / the posterior's concurrent split)."""
+
+    def __init__(self, block_off, split_frac=None, post_split_frac=None):
         off = np.ascontiguousarray(block_off, dtype=np.int64)
         if off.ndim != 1 or len(off) < 1 or off[0] != 0 or np.any(np.diff(off) < 0):
             raise ValueError("block offsets must start at 0 and be non-decreasing")
@@ -103,7 +106,10 @@ class Plan:
         self.nblocks = len(off) - 1
         self.total = int(off[-1])
         h = ctypes.c_void_p()
-        check(lib().itr_plan_create(ptr(off), self.nblocks, ctypes.byref(h)))
+        check(lib().itr_plan_create_ex(ptr(off), self.nblocks,
+                                       -1.0 if split_frac is None else float(split_frac),
+                                       -1.0 if post_split_frac is None else float(post_split_frac),
+                                       ctypes.byref(h)))
         self.handle = h.value
 
     def reserve(self, n: int, posterior: bool = False):

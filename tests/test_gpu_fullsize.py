@@ -5,8 +5,12 @@ do not need the CPU oracle to run over all of it:
   * the longest blocks (which the forward sweep splits into a forward and a backward half,
     meet in the middle) and a seeded sample of the rest against the oracle: log-likelihoods
     within 1e-8 relative, Viterbi paths identical;
-  * the split forward against the unsplit one on every split block (ITR_SPLIT_FRAC=0 at
-    plan creation): the same value to 1e-12 relative;
+  * the split forward against the unsplit one on every split block (split_frac=0 at plan
+    creation): the same value to 1e-12 relative;
+  * the combined call the bench times (itr_forward_viterbi: the CU-partitioned forward +
+    Viterbi) against the oracle on EVERY block: paths identical, log-likelihoods 1e-8; and
+    the same on BASELINE config 4's rank-0 shard at world size 8 (the chr100 layout, which
+    takes the other branches of the partition);
   * every block's log-likelihood finite and negative, the total equal to the block-order
     sum of the per-block values (loglik_wrapper semantics);
   * every posterior row sums to 1 (1e-12) and matches the oracle on the sampled blocks.
@@ -68,13 +72,53 @@ def test_full_size_sample_vs_oracle(full):
     np.testing.assert_array_equal(got, path_ref)
 
 
-def test_full_size_split_forward_matches_unsplit(full, monkeypatch):
-    monkeypatch.setenv("ITR_SPLIT_FRAC", "0")  # read by itr_plan_create
-    plan = hmm.Plan(full["off"])
+def test_full_size_split_forward_matches_unsplit(full):
+    plan = hmm.Plan(full["off"], split_frac=0)
     ll = hmm.forward_loglik_device(full["model"], plan, full["d_obs"]).cpu().numpy()
     k = full["longest"]
     np.testing.assert_allclose(full["ll"][k], ll[k], rtol=1e-12, atol=0)
     np.testing.assert_allclose(full["ll"], ll, rtol=1e-12, atol=0)
+
+
+def _check_all_blocks(t, obs, off, ll, path):
+    ll_ref = O.forward_loglik(t, obs, off)
+    np.testing.assert_allclose(ll, ll_ref, rtol=1e-8, atol=0)
+    path_ref = O.viterbi(t, obs, off)
+    bad = np.flatnonzero(path != path_ref)
+    assert bad.size == 0, f"{bad.size} columns differ, first at {bad[:5]}"
+
+
+def test_full_size_forward_viterbi_every_block(full):
+    """BASELINE config 2 exactly as bench.py times it: itr_forward_viterbi over all 10 M
+    columns (forward halves on reserved CUs beside the Viterbi long blocks, the per-wave
+    Viterbi on the others) against the CPU restatement on every block."""
+    plan = hmm.Plan(full["off"])
+    ll, path = hmm.forward_viterbi_device(full["model"], plan, full["d_obs"])
+    ll, path = ll.cpu().numpy(), path.cpu().numpy()
+    assert np.array_equal(path, full["path"])  # the separate calls' paths, bit for bit
+    np.testing.assert_allclose(ll, full["ll"], rtol=1e-12, atol=0)
+    _check_all_blocks(full["t"], full["obs"], full["off"], ll, path)
+
+
+def test_chr100_rank0_shard_forward_viterbi(gpu):
+    """BASELINE config 4's per-rank work at world size 8: the rank-0 shard of the fixed
+    100 Mbp alignment (bench.py --workload chr100: shard_ranges over the geometric block
+    layout, ~12.5 Mbp) through itr_forward_viterbi, every block against the oracle."""
+    import torch
+    from itrails_amd.distributed import shard_ranges
+    from itrails_amd.synth import sample_alignment_range
+    g = golden("model_kat_5_5.npz")
+    a, b, pi = g["a"], g["b"], g["pi"]
+    lengths = block_lengths(np.random.default_rng(12345), 100_000_000, 2000.0)
+    lo, hi = shard_ranges(lengths, 8)[0]
+    obs, off = sample_alignment_range(a, b, pi, lengths, lo, hi, seed=777)
+    assert 11_000_000 < off[-1] < 14_000_000
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).cuda()
+    ll, path = hmm.forward_viterbi_device(model, plan, d_obs)
+    _check_all_blocks(build_tables(a, b, pi), obs, off, ll.cpu().numpy(), path.cpu().numpy())
+    del d_obs, plan
+    torch.cuda.empty_cache()
 
 
 def test_full_size_loglik_properties(full):
@@ -104,18 +148,17 @@ def test_full_size_posterior_rows(full):
     torch.cuda.empty_cache()
 
 
-def test_full_size_posterior_split_matches_unsplit(full, monkeypatch):
+def test_full_size_posterior_split_matches_unsplit(full):
     """The posterior's concurrent forward/backward split (the longest blocks' backward
     sweeps run beside the forward sweep, post_combine_kernel joins the stored rows) against
-    the two-pass sweep (ITR_POST_SPLIT_FRAC=0 at plan creation) on every row, and the
+    the two-pass sweep (post_split_frac=0 at plan creation) on every row, and the
     longest blocks against the CPU restatement."""
     import torch
     n = full["a"].shape[0]
     plan = hmm.Plan(full["off"])
     plan.reserve(n, posterior=True)
     post = hmm.posterior_device(full["model"], plan, full["d_obs"])
-    monkeypatch.setenv("ITR_POST_SPLIT_FRAC", "0")
-    plan0 = hmm.Plan(full["off"])
+    plan0 = hmm.Plan(full["off"], post_split_frac=0)
     plan0.reserve(n, posterior=True)
     post0 = hmm.posterior_device(full["model"], plan0, full["d_obs"])
     assert float((post - post0).abs().max()) < 1e-12
