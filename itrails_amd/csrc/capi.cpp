@@ -108,8 +108,6 @@ struct Partition {
   hipStream_t lng = nullptr, lng2 = nullptr;  // the reserved CUs
   hipStream_t blk = nullptr;                   // the other CUs
   hipEvent_t fork = nullptr, jl = nullptr, jl2 = nullptr, jb = nullptr;
-  hipStream_t blk2 = nullptr;  // experiment builds: a second stream on the other CUs
-  hipEvent_t jb2 = nullptr;
   std::vector<uint32_t> mb;    // the other CUs' mask
 };
 // The calling thread's partitions; destroyed with the thread (each thread that decodes owns
@@ -121,9 +119,9 @@ struct Partitions {
     const bool have_dev = hipGetDevice(&dev) == hipSuccess;
     for (auto& x : v) {
       (void)hipSetDevice(x.device);
-      for (hipStream_t* q : {&x.lng, &x.lng2, &x.blk, &x.blk2})
+      for (hipStream_t* q : {&x.lng, &x.lng2, &x.blk})
         if (*q) (void)hipStreamDestroy(*q);
-      for (hipEvent_t* e : {&x.fork, &x.jl, &x.jl2, &x.jb, &x.jb2})
+      for (hipEvent_t* e : {&x.fork, &x.jl, &x.jl2, &x.jb})
         if (*e) (void)hipEventDestroy(*e);
     }
     v.clear();
@@ -185,8 +183,11 @@ struct itr_model {
   // log E with rows padded to the one-block-per-wave Viterbi layout's width (-inf columns),
   // when that layout serves this state count (wave_vit.hip)
   double* LEW = nullptr;
-  double* EW = nullptr;  // E likewise (zero columns) plus a row of ones (row 625)
   int xrw = 0;
+  // E padded to the per-wave matrix-core forward's width (zero columns) plus a row of ones
+  // (row 625), when that layout serves this state count (wave_tasks.h)
+  double* EF = nullptr;
+  int erf = 0;
 };
 
 struct itr_plan {
@@ -217,6 +218,16 @@ struct itr_plan {
   // utasks + matrix-core groups of task ids into mtasks (split slots hsplit_blk); posterior =
   // VALU blocks order[0, nurg) + groups of four consecutive blocks of order[nurg, nblocks),
   // nurg chosen per call from the state count (MfmaGeometry.pfrac)
+  // per-wave matrix-core forward (wave_tasks.h): groups of four ids of `tasks`
+  int64_t nwgroups = 0;
+  int32_t* d_wgroups = nullptr;
+  // Viterbi placement (viterbi_impl): the vit_nlong longest blocks (vit_long_cols columns)
+  // on the 9-wave layout; the combined call's mixed queue (wave_sweeps.hip): entries >= 0 =
+  // Viterbi blocks, < 0 = forward groups of groups_ll, by expected duration; tasks at least
+  // mix_prio_* long run at raised wave priority
+  int64_t vit_nlong = 0, vit_long_cols = 0, nmix = 0;
+  int32_t* d_mix = nullptr;
+  int mix_prio_fwd = INT32_MAX, mix_prio_vit = INT32_MAX;
   int64_t nutasks = 0, ngroups_ll = 0, nhsplit = 0;
   int32_t *d_utasks = nullptr, *d_mtasks = nullptr, *d_groups_ll = nullptr,
           *d_hsplit_blk = nullptr;
@@ -252,16 +263,16 @@ int check_plan(itr_plan_t p) {
 
 // Workspace: Viterbi = one checkpoint row (f64) and one flag word (u16) per state per
 // 16-column tile record; posterior = the forward rows of every column.
-int vit_stride(int n) {  // record stride of the Viterbi workspace for this state count
+int vit_stride(int n) {
   const itr::WaveVitGeometry wv = itr::wave_vit_geometry(n);
-  bool wave = wv.iq > 0;
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_NO_WAVE")) wave = false;
-#endif
-  if (wave) return wv.xr;
-  const itr::VitHybridGeometry vh = itr::vit_hybrid_geometry(n);
-  return vh.cfg >= 0 ? vh.xr : itr::sweep_row_stride(n, itr::MODE_VIT);
+  return wv.iq > 0 ? wv.xr : itr::sweep_row_stride(n, itr::MODE_VIT);
 }
+
+// Measured per-column costs of the two Viterbi layouts at N = 70: a block
+// alone on its CU in the 9-wave layout steps in ~325 ns; the per-wave sweep on a loaded CU
+// costs ~114 CU-ns per column.  They decide whether the CU partition pays (viterbi_impl).
+constexpr double kVitLoneNs = 325e-9;
+constexpr double kVitWaveCuNs = 114e-9;
 
 // The posterior's concurrent split (launch_post_split): only on the VALU-only posterior
 // (no matrix-core form at this state count) and only where the blocks are few
@@ -487,21 +498,28 @@ int itr_model_create(int n, const double* a, const double* la, const double* E,
     if (!e && hipMemcpy(m->LEW, lew.data(), lew.size() * sizeof(double),
                         hipMemcpyHostToDevice) != hipSuccess)
       e = fail(ITR_EHIP, "table upload failed");
-#ifdef ITR_EXPERIMENT  // the per-wave forward's table (experiment builds only)
-    std::vector<double> ew((size_t)(ITR_NOBS + 1) * w, 0.0);
-    for (int o = 0; o < ITR_NOBS; ++o)
-      for (int j = 0; j < n; ++j) ew[(size_t)o * w + j] = E[(size_t)o * n + j];
-    for (int j = 0; j < w; ++j) ew[(size_t)ITR_NOBS * w + j] = 1.0;
-    if (!e) e = dev_alloc(&m->EW, ew.size());
-    if (!e && hipMemcpy(m->EW, ew.data(), ew.size() * sizeof(double),
-                        hipMemcpyHostToDevice) != hipSuccess)
-      e = fail(ITR_EHIP, "table upload failed");
-#endif
     if (e) {
       itr_model_destroy(m);
       return e;
     }
     m->xrw = w;
+  }
+  const itr::WaveMfmaGeometry wf = itr::wave_mfma_geometry(n);
+  if (wf.cfg >= 0) {
+    const int w = wf.er;
+    std::vector<double> ef((size_t)(ITR_NOBS + 1) * w, 0.0);
+    for (int o = 0; o < ITR_NOBS; ++o)
+      for (int j = 0; j < n; ++j) ef[(size_t)o * w + j] = E[(size_t)o * n + j];
+    for (int j = 0; j < w; ++j) ef[(size_t)ITR_NOBS * w + j] = 1.0;
+    e = dev_alloc(&m->EF, ef.size());
+    if (!e && hipMemcpy(m->EF, ef.data(), ef.size() * sizeof(double), hipMemcpyHostToDevice) !=
+                  hipSuccess)
+      e = fail(ITR_EHIP, "table upload failed");
+    if (e) {
+      itr_model_destroy(m);
+      return e;
+    }
+    m->erf = w;
   }
   *out = m;
   return 0;
@@ -517,7 +535,7 @@ int itr_model_destroy(itr_model_t m) {
   dev_free(m->LPIE);
   dev_free(m->aT);
   dev_free(m->LEW);
-  dev_free(m->EW);
+  dev_free(m->EF);
   delete m;
   return 0;
 }
@@ -629,6 +647,27 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
     return sorted;
   };
   std::vector<int32_t> tasks = make_tasks(nblocks);
+  // groups of four `tasks` ids for the per-wave matrix-core forward: forward-shaped tasks and
+  // backward halves apart (a group shares its matrix operand), each kind longest first (the
+  // task list is sorted longest first)
+  std::vector<int32_t> wgroups;
+  {
+    std::vector<int32_t> fw, bw;
+    for (int64_t k = 0; k < (int64_t)tasks.size() / 3; ++k)
+      (tasks[3 * k + 1] < 0 ? bw : fw).push_back((int32_t)k);
+    auto tlen = [&](int32_t k) {
+      const int32_t b = tasks[3 * k], sp = tasks[3 * k + 1];
+      const int64_t Tb = h_off[b + 1] - h_off[b];
+      return sp > 0 ? (int64_t)sp : (sp < 0 ? Tb + sp + 1 : Tb);
+    };
+    size_t fi = 0, bi = 0;
+    while (fi < fw.size() || bi < bw.size()) {
+      const bool pick_f = bi >= bw.size() || (fi < fw.size() && tlen(fw[fi]) >= tlen(bw[bi]));
+      auto& v = pick_f ? fw : bw;
+      size_t& i = pick_f ? fi : bi;
+      for (int r = 0; r < 4; ++r) wgroups.push_back(i < v.size() ? v[i++] : -1);
+    }
+  }
   // Hybrid sweeps (mfma_sweeps.hip).  A matrix-core group steps four blocks in about twice
   // the VALU step time, so the longest work stays on the lower-latency VALU path and the
   // bulk goes through the matrix cores.  Forward log-likelihood, with
@@ -703,6 +742,53 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
       }
     }
   }
+  // Viterbi long set: blocks longer than 0.45 x the longest and >= 2,048 columns (a lone
+  // per-wave block steps ~2x slower than one in the 9-wave layout)
+  {
+    double lfrac = 0.45;
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_VIT_LONG_FRAC")) lfrac = atof(getenv("ITR_VIT_LONG_FRAC"));
+#endif
+    int64_t k = 0, cols = 0;
+    while (k < nblocks && p->sorted_len[k] >= 2048 && (double)p->sorted_len[k] > lfrac * (double)tmax)
+      cols += p->sorted_len[k++];
+    p->vit_nlong = k;
+    p->vit_long_cols = cols;
+  }
+  // The mixed queue: forward groups (steps = their longest member) and the remaining Viterbi
+  // blocks merged by expected duration, longest first.  Measured per-column step times under
+  // full load at N = 70: a forward group ~0.92 us, a per-wave Viterbi block ~0.64 us.
+  std::vector<int32_t> mix;
+  {
+    const int64_t ng = (int64_t)groups_ll.size() / 4;
+    std::vector<int64_t> gsteps(ng, 0);
+    for (int64_t g = 0; g < ng; ++g)
+      for (int r = 0; r < 4; ++r) {
+        const int32_t id = groups_ll[4 * g + r];
+        if (id < 0) continue;
+        const int32_t b = mtasks[3 * id], sp = mtasks[3 * id + 1];
+        const int64_t Tb = h_off[b + 1] - h_off[b];
+        gsteps[g] = std::max(gsteps[g], sp > 0 ? (int64_t)sp : (sp < 0 ? Tb + sp + 1 : Tb));
+      }
+    std::vector<int64_t> gidx(ng);
+    std::iota(gidx.begin(), gidx.end(), 0);
+    std::stable_sort(gidx.begin(), gidx.end(), [&](int64_t x, int64_t y) { return gsteps[x] > gsteps[y]; });
+    const double cf = 0.92, cv = 0.64;
+    int64_t gi = 0, vi = p->vit_nlong;
+    const int64_t nprio = 512;  // about one per SIMD pair of the GPU
+    while (gi < ng || vi < nblocks) {
+      const bool take_f = vi >= nblocks ||
+                          (gi < ng && cf * (double)gsteps[gidx[gi]] >= cv * (double)p->sorted_len[vi]);
+      if ((int64_t)mix.size() == nprio) {
+        p->mix_prio_fwd = (int)std::max<int64_t>(1, gi < ng ? gsteps[gidx[gi]] : 1);
+        p->mix_prio_vit = (int)std::max<int64_t>(1, vi < nblocks ? p->sorted_len[vi] : 1);
+      }
+      if (take_f) mix.push_back(-(int32_t)gidx[gi++] - 1);
+      else mix.push_back(order[vi++]);
+    }
+    p->nmix = (int64_t)mix.size();
+  }
+  p->nwgroups = (int64_t)wgroups.size() / 4;
   p->nutasks = (int64_t)utasks.size() / 3;
   p->ngroups_ll = (int64_t)groups_ll.size() / 4;
   p->nhsplit = (int64_t)hsplit_blk.size();
@@ -710,6 +796,8 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
   p->nsplit = (int64_t)split_blk.size();
   int e = 0;
   if (!e) e = dev_alloc(&p->d_tasks, tasks.size());
+  if (!e) e = dev_alloc(&p->d_wgroups, wgroups.size());
+  if (!e) e = dev_alloc(&p->d_mix, mix.size());
   if (!e) e = dev_alloc(&p->d_utasks, utasks.size());
   if (!e) e = dev_alloc(&p->d_mtasks, mtasks.size());
   if (!e) e = dev_alloc(&p->d_groups_ll, groups_ll.size());
@@ -740,6 +828,8 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
   up(p->d_boff, boff.data(), nblocks * sizeof(int64_t));
   up(p->d_order, order.data(), nblocks * sizeof(int32_t));
   up(p->d_tasks, tasks.data(), tasks.size() * sizeof(int32_t));
+  up(p->d_wgroups, wgroups.data(), wgroups.size() * sizeof(int32_t));
+  up(p->d_mix, mix.data(), mix.size() * sizeof(int32_t));
   up(p->d_utasks, utasks.data(), utasks.size() * sizeof(int32_t));
   up(p->d_mtasks, mtasks.data(), mtasks.size() * sizeof(int32_t));
   up(p->d_groups_ll, groups_ll.data(), groups_ll.size() * sizeof(int32_t));
@@ -765,6 +855,8 @@ int itr_plan_destroy(itr_plan_t p) {
   dev_free(p->d_sink);
   dev_free(p->d_stay);
   dev_free(p->d_tasks);
+  dev_free(p->d_wgroups);
+  dev_free(p->d_mix);
   dev_free(p->d_utasks);
   dev_free(p->d_mtasks);
   dev_free(p->d_groups_ll);
@@ -811,6 +903,38 @@ int itr_forward_loglik(itr_model_t m, itr_plan_t p, const uint16_t* obs, double*
     return fail(ITR_ESTATE, "forward task tables missing");
   const itr::MfmaGeometry g = itr::mfma_geometry(m->n, itr::MODE_FWD_LL);
   int xr = itr::sweep_row_stride(m->n, itr::MODE_FWD_LL);
+#ifdef ITR_EXPERIMENT
+  const itr::WaveMfmaGeometry wf = itr::wave_mfma_geometry(m->n);
+  if (getenv("ITR_WAVE_FWD") && wf.cfg >= 0 && m->EF && p->nwgroups > 0) {
+    itr::WaveMfmaArgs w{};
+    w.n = m->n;
+    w.ngroups = p->nwgroups;
+    w.groups = p->d_wgroups;
+    w.tasks = p->d_tasks;
+    w.queue = p->d_queue + 11;
+    w.off = p->d_off;
+    w.obs = obs;
+    w.a = m->a;
+    w.aT = m->aT;
+    w.ef = m->EF;
+    w.emit = m->E;
+    w.init = m->PIE;
+    w.loglik = loglik;
+    w.svec = p->d_svec;
+    w.sstride = wf.er;
+    w.sK = p->d_sK;
+    w.prio_len = INT32_MAX;
+    const int64_t grid = std::min<int64_t>((int64_t)wf.per_cu * cu_count(), (p->nwgroups + 3) / 4);
+    HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), st));
+    {
+      Scope sc("forward", st);
+      HIP_TRY(itr::launch_wave_mfma(wf, (int)grid, w, st));
+    }
+    HIP_TRY(itr::launch_fwd_split_combine(m->n, wf.er, (int)p->nsplit, p->d_split_blk, p->d_svec,
+                                          p->d_sK, loglik, st));
+    return 0;
+  }
+#endif
   if (g.cfg >= 0 && p->ngroups_ll > 0) {
     a.tasks = p->d_utasks;
     a.nblocks = p->nutasks;
@@ -831,6 +955,19 @@ namespace {
 
 // The Viterbi sweep and traceback of every block into `path`; with fwd_loglik, the forward
 // log-likelihood sweep too, overlapped with the Viterbi sweep's longest blocks.
+//
+// Work placement.  A block's sweep is a strictly sequential chain, so the
+// longest blocks need the lowest step latency and the bulk the highest throughput:
+//   * the longest blocks' Viterbi (longer than 0.45 x the longest, >= 2,048 columns): the
+//     9-wave VALU layout, one workgroup per CU, on `reserve` CUs (CU-masked stream lng);
+//   * with the forward: its latency-bound VALU tasks (halves of the longest blocks) on rf of
+//     those reserved CUs (lng2), and on the other CUs (blk) ONE persistent launch of
+//     per-wavefront tasks from a single queue ordered by expected duration: forward groups
+//     of four tasks on the matrix cores and one Viterbi block per wave (wave_sweeps.hip);
+//   * without the mixed launch (other state counts): the forward's matrix-core groups, then
+//     the per-wave Viterbi on blk.
+// When the long blocks would keep the reserved CUs busy longer than the rest keeps the
+// others (few, equally long blocks), every block goes to the 9-wave layout on all CUs.
 int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
                  hipStream_t st, double* fwd_loglik) {
   if (int e = reserve(p, m->n, true, false)) return e;
@@ -845,43 +982,22 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   a.stay = p->d_stay;
   a.last_state = p->d_last;
   const itr::WaveVitGeometry wv = itr::wave_vit_geometry(m->n);
-  const itr::VitHybridGeometry vh = itr::vit_hybrid_geometry(m->n);
   bool wave = wv.iq > 0 && m->LEW && m->xrw == wv.xr;
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_NO_WAVE")) wave = false;
-#endif
-  // The longest blocks (longer than lfrac x the longest, at least 2,048 columns) on the
-  // 9-wave VALU layout on `reserve_cus` reserved CUs; the rest one block per wavefront on the
-  // other CUs (a lone wave steps ~2x slower, so the per-wave sweep must not get blocks
-  // longer than ~half the longest).  When the long blocks would keep the reserved CUs busy
-  // longer than the rest keeps the others (workloads of few, equally long blocks), every
-  // block goes to the 9-wave layout on all CUs.
   const int cus = cu_count();
   int reserve_cus = cus / 4;
-  double lfrac = 0.45;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_VIT_RESERVE")) reserve_cus = atoi(getenv("ITR_VIT_RESERVE"));
-  if (getenv("ITR_VIT_LONG_FRAC")) lfrac = atof(getenv("ITR_VIT_LONG_FRAC"));
 #endif
   reserve_cus = std::max(1, std::min(reserve_cus, cus - 1));
-  int64_t nlong = 0;
+  const int64_t nlong = wave ? p->vit_nlong : 0;
   if (wave) {
-    const int64_t tmax = p->sorted_len[0];
-    int64_t cum = 0;
-    while (nlong < p->nblocks && p->sorted_len[nlong] >= 2048 &&
-           (double)p->sorted_len[nlong] > lfrac * (double)tmax) {
-      cum += p->sorted_len[nlong];
-      ++nlong;
-    }
-    // Keep the partition when the reserved CUs finish the long blocks no later than the other
-    // CUs finish the rest (or than the longest block alone).  Measured at N = 70: ~325 ns per
-    // column for a block alone on its CU in the 9-wave layout; ~114 CU-ns per column for the
-    // per-wave sweep on a loaded CU (5.3 ms for 8.9 M columns on 192 CUs).
-    auto t_long = [&](int64_t c) { return (double)c * 325e-9 / reserve_cus; };
-    auto t_bulk = [&](int64_t c) { return (double)(p->total - c) * 114e-9 / (cus - reserve_cus); };
-    // (moving more long blocks to the reserved CUs until both sides balance by this estimate
-    // was measured slower: chr10 Viterbi 5.65 -> 6.43 ms, chr100 47.6 -> 50.6 ms)
-    if (t_long(cum) > 1.1 * std::max(t_bulk(cum), (double)tmax * 325e-9)) wave = false;
+    // Keep the partition when the reserved CUs finish the long blocks no later than the
+    // other CUs finish the rest (or than the longest block alone), by the measured per-column
+    // costs (plan: vit_lone_ns for a block alone on its CU in the 9-wave layout,
+    // vit_wave_cu_ns CU-ns per column of the per-wave sweep on a loaded CU)
+    const double t_long = (double)p->vit_long_cols * kVitLoneNs / reserve_cus;
+    const double t_bulk = (double)(p->total - p->vit_long_cols) * kVitWaveCuNs / (cus - reserve_cus);
+    if (t_long > 1.1 * std::max(t_bulk, (double)p->sorted_len[0] * kVitLoneNs)) wave = false;
   }
   if (!wave && fwd_loglik)  // no overlap: the forward sweep first, on the caller's stream
     if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, st)) return e;
@@ -907,22 +1023,16 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     std::optional<Scope> sc;
     if (!fwd_loglik) sc.emplace("viterbi", st);
     Partition* pt = nullptr;
-    // with the forward sweep: its VALU tasks (the halves of the longest blocks, latency-bound)
-    // beside the Viterbi long blocks on the reserved CUs, its matrix-core groups on the others
     const itr::MfmaGeometry gf = itr::mfma_geometry(m->n, itr::MODE_FWD_LL);
-    // (experiment builds: ITR_FV_WAVE_FWD=1 runs the forward in the per-wave layout on the
-    // other CUs before the per-wave Viterbi instead; measured slower, wave_vit.hip)
-    bool wave_fwd = false;
+    const itr::WaveMfmaGeometry wf = itr::wave_mfma_geometry(m->n);
+    // the forward's VALU tasks (halves of the longest blocks) on rf reserved CUs; they must
+    // not outnumber the reserved CUs
+    const bool split_fwd = fwd_loglik && nlong > 0 && gf.cfg >= 0 && p->ngroups_ll > 0 &&
+                           p->nutasks > 0 && p->nutasks < reserve_cus;
+    bool mixed = split_fwd && wf.mixed && m->EF && p->nmix > 0;
 #ifdef ITR_EXPERIMENT
-    wave_fwd = fwd_loglik && m->EW && p->ntasks > 0 && getenv("ITR_FV_WAVE_FWD");
+    if (getenv("ITR_NO_MIXED")) mixed = false;
 #endif
-    // (the VALU halves must not outnumber the reserved CUs; experiment builds: ITR_FV_SPLIT_CAP)
-    int64_t split_cap = reserve_cus;
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_FV_SPLIT_CAP")) split_cap = atoi(getenv("ITR_FV_SPLIT_CAP"));
-#endif
-    const bool split_fwd = fwd_loglik && !wave_fwd && nlong > 0 && gf.cfg >= 0 &&
-                           p->ngroups_ll > 0 && p->nutasks > 0 && p->nutasks < split_cap;
     itr::SweepArgs af = base_args(m, p, obs);
     af.mat = m->a;
     af.matT = m->aT;
@@ -937,7 +1047,8 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     if (split_fwd) {
       rf = std::min<int64_t>(p->nutasks, 3 * reserve_cus / 8);
 #ifdef ITR_EXPERIMENT
-      if (getenv("ITR_FWD_RESERVE")) rf = std::min<int64_t>(atoi(getenv("ITR_FWD_RESERVE")), reserve_cus - 1);
+      if (getenv("ITR_FWD_RESERVE"))
+        rf = std::min<int64_t>(atoi(getenv("ITR_FWD_RESERVE")), reserve_cus - 1);
 #endif
       HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
       HIP_TRY(hipMemsetAsync(p->d_queue + 8, 0, 2 * sizeof(int), st));  // the idle loops' counters
@@ -957,60 +1068,45 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       }
     }
     hipStream_t sb = pt ? pt->blk : st;
-    if (wave_fwd) {
-      itr::WaveFwdArgs f{};
+    const int ocus = cus - (pt ? reserve_cus : 0);  // CUs of the sb launches
+    if (mixed) {
+      // forward groups (the hybrid plan's matrix-core tasks) and the per-wave Viterbi blocks
+      // from one queue ordered by expected duration (plan: mix list)
+      itr::WaveMfmaArgs f{};
       f.n = m->n;
-      f.xr = wv.xr;
-      f.ntasks = p->ntasks;
-      f.tasks = p->d_tasks;
-      f.queue = p->d_queue + 10;
+      f.ngroups = p->ngroups_ll;
+      f.groups = p->d_groups_ll;
+      f.tasks = p->d_mtasks;
       f.off = p->d_off;
       f.obs = obs;
       f.a = m->a;
       f.aT = m->aT;
-      f.ew = m->EW;
+      f.ef = m->EF;
       f.emit = m->E;
       f.init = m->PIE;
       f.loglik = fwd_loglik;
       f.svec = p->d_svec;
+      f.sstride = gf.xr;
       f.sK = p->d_sK;
-      f.prio_len = w.prio_len;
-      const int64_t grid = std::min<int64_t>(
-          (int64_t)wv.per_cu * (cus - (pt ? reserve_cus : 0)), (p->ntasks + 3) / 4);
-      HIP_TRY(hipMemsetAsync(f.queue, 0, sizeof(int), sb));
-      HIP_TRY(itr::launch_wave_fwd(wv, (int)grid, f, sb));
-    } else if (split_fwd) {
-      if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, sb, nullptr, false, true,
-                             (int64_t)gf.per_cu * (cus - reserve_cus), false))
-        return e;
-    } else if (fwd_loglik) {
-      if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, sb)) return e;
-    }
-    hipStream_t sw = sb;  // the per-wave sweep: after the forward's matrix-core groups
-    int wave_per_cu = wv.per_cu;
-#ifdef ITR_EXPERIMENT
-    // ... or beside them on a fourth stream (needs GPU_MAX_HW_QUEUES >= 5)
-    if (split_fwd && getenv("ITR_FV_BESIDE")) {
-      if (!pt->blk2) {
-        HIP_TRY(hipExtStreamCreateWithCUMask(&pt->blk2, (uint32_t)pt->mb.size() * 32,
-                                             pt->mb.data()));
-        HIP_TRY(hipEventCreateWithFlags(&pt->jb2, hipEventDisableTiming));
+      f.prio_len = p->mix_prio_fwd;
+      w.prio_len = p->mix_prio_vit;
+      const int64_t grid = std::min<int64_t>((int64_t)wf.mixed_per_cu * ocus, (p->nmix + 3) / 4);
+      HIP_TRY(hipMemsetAsync(p->d_queue + 12, 0, sizeof(int), sb));
+      HIP_TRY(itr::launch_wave_mixed(wf, (int)grid, w, f, p->d_mix, (int)p->nmix,
+                                     p->d_queue + 12, sb));
+    } else {
+      if (split_fwd) {
+        if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, sb, nullptr, false, true,
+                               (int64_t)gf.per_cu * ocus, false))
+          return e;
+      } else if (fwd_loglik) {
+        if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, sb)) return e;
       }
-      sw = pt->blk2;
-      HIP_TRY(hipStreamWaitEvent(sw, pt->fork, 0));
-      wave_per_cu = atoi(getenv("ITR_FV_BESIDE"));
-    }
-#endif
-    if (w.nblocks > 0) {
-      const int64_t work = (w.nblocks + 3) / 4;
-      const int64_t grid =
-          std::min<int64_t>((int64_t)wave_per_cu * (cus - (pt ? reserve_cus : 0)), work);
-      HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), sw));
-      HIP_TRY(itr::launch_wave_vit(wv, (int)grid, w, sw));
-    }
-    if (sw != sb) {
-      HIP_TRY(hipEventRecord(pt->jb2, sw));
-      HIP_TRY(hipStreamWaitEvent(st, pt->jb2, 0));
+      if (w.nblocks > 0) {  // the per-wave sweep: after the forward's matrix-core groups
+        const int64_t grid = std::min<int64_t>((int64_t)wv.per_cu * ocus, (w.nblocks + 3) / 4);
+        HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), sb));
+        HIP_TRY(itr::launch_wave_vit(wv, (int)grid, w, sb));
+      }
     }
     if (pt) {
       HIP_TRY(hipEventRecord(pt->jl, pt->lng));
@@ -1025,35 +1121,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     if (split_fwd)  // log P of the split blocks from their two halves
       HIP_TRY(itr::launch_fwd_split_combine(m->n, gf.xr, (int)p->nhsplit, p->d_hsplit_blk,
                                             p->d_svec, p->d_sK, fwd_loglik, st));
-    if (wave_fwd)
-      HIP_TRY(itr::launch_fwd_split_combine(m->n, wv.xr, (int)p->nsplit, p->d_split_blk,
-                                            p->d_svec, p->d_sK, fwd_loglik, st));
-  } else if (vh.cfg >= 0) {
-    // the longest blocks (longer than vfrac x the longest) as VALU tasks, the rest in
-    // lock-step groups; one workgroup per CU
-    double vfrac = 0.35;
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_VIT_URGENT_FRAC")) vfrac = atof(getenv("ITR_VIT_URGENT_FRAC"));
-#endif
-    const double lim = std::max(512.0, vfrac * (double)p->sorted_len[0]);
-    int64_t nurg = 0;
-    while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
-    a.queue = p->d_queue + 5;
-    a.prio_len = 0;
-    const int64_t work = nurg + (p->nblocks - nurg + vh.G - 1) / vh.G;
-    const int64_t grid = std::min<int64_t>((int64_t)vh.per_cu * cu_count(), work);
-    HIP_TRY(hipMemsetAsync(p->d_queue + 5, 0, 2 * sizeof(int), st));
-    Scope sc("viterbi", st);
-    HIP_TRY(itr::launch_vit_hybrid(vh, (int)grid, a, (int)nurg, p->d_cubusy, st));
   } else {
-#ifdef ITR_EXPERIMENT
-    // blocks longer than frac x the longest decode alone on their CU
-    if (getenv("ITR_VIT_EXCL_FRAC")) {
-      a.cu_busy = p->d_cubusy;
-      a.excl_len = std::max<int64_t>(1, (int64_t)(atof(getenv("ITR_VIT_EXCL_FRAC")) *
-                                                  (double)p->sorted_len[0]));
-    }
-#endif
     if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
   }
   both.reset();

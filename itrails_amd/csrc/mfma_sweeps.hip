@@ -169,16 +169,22 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
     if (Tmax > 0) {
       const bool urgent = Tmax >= p.prio_len;
       if (urgent) __builtin_amdgcn_s_setprio(2);
-      // symbol of step s of this lane's row: column s (forward) or Tb - 1 - s (backward),
-      // clamped into the block; -2 = a row of ones (a backward half's last step)
+      // Prefetch with no load consumed inside its own tile: the symbol of step s of this
+      // lane's row (column s forward, Tb - 1 - s backward, clamped into the block; an empty
+      // row reads column 0 of the array) is loaded raw two tiles ahead, unconditionally;
+      // one tile ahead its emission value is loaded from the address it gives (padded target
+      // lanes read column 0: finite, and their products are 0); a backward half's last step
+      // (a row of ones) is applied where the value is used.  A clamp or a select on a fresh
+      // load makes hipcc wait for it on the spot (s_waitcnt vmcnt(0) every column).
       auto sym = [&](int gb, int s) -> int {
-        if (MODE == MODE_FWD_LL && task_split[gb] < 0 && s == T[gb] - 1) return -2;
         const int t = dir[gb] > 0 ? s : Tb[gb] - 1 - s;
         const int tc = min(max(t, 0), max(Tb[gb] - 1, 0));
-        return Tb[gb] > 0 ? min((int)p.obs[c0[gb] + tc], 624) : 0;
+        return (int)p.obs[Tb[gb] > 0 ? c0[gb] + tc : 0];
       };
-      auto emis = [&](int sy) -> double {
-        return jv ? (sy < 0 ? 1.0 : p.emit[sy * n + j]) : 0.0;
+      const int jc = jv ? j : 0;
+      auto emis = [&](int sy) -> double { return p.emit[min(sy, 624) * n + jc]; };
+      auto ones_at = [&](int gb, int s) -> bool {
+        return MODE == MODE_FWD_LL && task_split[gb] < 0 && s == T[gb] - 1;
       };
       int snxt[GB][TE];
       double enxt[GB][TE];
@@ -191,7 +197,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
         for (int gb = 0; gb < GB; ++gb) {
           // x_0 = pi * e_0 (forward rows); a backward half starts from e_{Tb-1}
           const double* x0tab = dir[gb] < 0 ? p.emit : p.init;
-          x[gb] = (T[gb] > 0 && jv) ? x0tab[sym(gb, 0) * n + j] : 0.0;
+          x[gb] = (T[gb] > 0 && jv) ? x0tab[min(sym(gb, 0), 624) * n + j] : 0.0;
           if (jv) X[gb][0][r][j] = x[gb];
           if (MODE == MODE_FWD_STORE && T[gb] > 0) p.alpha[c0[gb] * p.astride + j] = x[gb];
           xfin[gb] = x[gb];
@@ -248,7 +254,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
                     K[gb] += e;
                   }
                 }
-                x[gb] = (y[gb] * ecur[gb][sub]) * sc;
+                x[gb] = (y[gb] * (ones_at(gb, t) ? 1.0 : ecur[gb][sub])) * sc;
                 if constexpr (MODE == MODE_FWD_LL) {
                   if (t == T[gb] - 1) {
                     xfin[gb] = x[gb];
@@ -303,16 +309,18 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
         // Step s handles column t = T - 1 - s of every block of the group.
         double bt[GB];
         double anxt[GB][TE];
-        auto arow = [&](int gb, int s) -> double {  // stored forward row of column T-1-s
+        // stored forward row of column T-1-s (unconditional load, see above: an empty row
+        // reads row 0; padded target lanes read stored zeros)
+        auto arow = [&](int gb, int s) -> double {
           const int tc = max(T[gb] - 1 - s, 0);
-          return (T[gb] > 0 && jv) ? p.alpha[(c0[gb] + tc) * p.astride + j] : 0.0;
+          return p.alpha[(T[gb] > 0 ? c0[gb] + tc : 0) * p.astride + j];
         };
 #pragma unroll
         for (int gb = 0; gb < GB; ++gb) {
           bt[gb] = (T[gb] > 0 && jv) ? 1.0 : 0.0;
 #pragma unroll
           for (int u = 0; u < TE; ++u) {
-            enxt[gb][u] = jv ? p.emit[sym(gb, T[gb] - 1 - u) * n + j] : 0.0;
+            enxt[gb][u] = emis(sym(gb, T[gb] - 1 - u));
             anxt[gb][u] = arow(gb, u);
             snxt[gb][u] = sym(gb, T[gb] - 1 - (TE + u));
           }
@@ -329,7 +337,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
             }
 #pragma unroll
             for (int u = 0; u < TE; ++u) {
-              enxt[gb][u] = jv ? p.emit[snxt[gb][u] * n + j] : 0.0;
+              enxt[gb][u] = emis(snxt[gb][u]);
               anxt[gb][u] = arow(gb, s0 + TE + u);
               snxt[gb][u] = sym(gb, T[gb] - 1 - (s0 + 2 * TE + u));
             }

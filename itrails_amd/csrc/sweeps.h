@@ -116,23 +116,7 @@ MfmaGeometry mfma_geometry(int n, int mode);
 hipError_t launch_hybrid_sweep(int mode, const MfmaGeometry& g, int grid, const MfmaArgs& a,
                                const SweepArgs& v, hipStream_t st);
 
-// Viterbi hybrid (vit_hybrid.hip): the longest blocks as VALU tasks, the bulk as groups of
-// G blocks in lock-step, two lanes per (block, target)
-struct VitHybridGeometry {
-  int cfg;      // configuration (negative: none for this n)
-  int block;    // threads per workgroup
-  int xr;       // record stride of the checkpoint rows / flag words
-  int G;        // blocks per lock-step group
-  size_t lds;   // dynamic LDS bytes
-  int per_cu;   // resident workgroups per CU
-};
-VitHybridGeometry vit_hybrid_geometry(int n);
-// v.order[0, nurg) as VALU tasks, then groups of v.order[nurg, v.nblocks); v.queue[0..1]
-// cu_busy: [4096] per-CU counts of long blocks in progress (zero between launches)
-hipError_t launch_vit_hybrid(const VitHybridGeometry& g, int grid, const SweepArgs& v, int nurg,
-                             int* cu_busy, hipStream_t st);
-
-// Viterbi with one block per wavefront (wave_vit.hip)
+// Viterbi with one block per wavefront (wave_tasks.h, wave_sweeps.hip)
 struct VitArgs {
   int n;                        // hidden states
   int xr;                       // record stride of the checkpoint rows / flag words
@@ -157,30 +141,50 @@ struct WaveVitGeometry {
   size_t lds;   // dynamic LDS bytes
   int per_cu;   // resident workgroups per CU
 };
-// the forward log-likelihood sweep in the same layout (wave_vit.hip): the VALU sweep's tasks
-struct WaveFwdArgs {
+WaveVitGeometry wave_vit_geometry(int n);
+hipError_t launch_wave_vit(const WaveVitGeometry& g, int grid, const VitArgs& p,
+                           hipStream_t st);
+
+// The forward log-likelihood sweep with one group of four tasks per wavefront on the matrix
+// cores (wave_fwd.hip): the throughput form for short tasks
+struct WaveMfmaArgs {
   int n;                        // hidden states
-  int xr;                       // stride of the split halves' vectors in svec
-  int64_t ntasks;
-  const int32_t* tasks;         // [ntasks x 3] {block, split, slot}, longest first (capi.cpp)
+  int64_t ngroups;
+  const int32_t* groups;        // [ngroups x 4] task ids (-1: none), longest first; a group is
+                                //   all forward-shaped tasks or all backward halves
+  const int32_t* tasks;         // {block, split, slot} (SweepArgs.tasks)
   int* queue;                   // work counter, zero at launch
   const int64_t* off;           // [plan blocks + 1]
   const uint16_t* obs;          // [total]
   const double* a;              // a, n x n
-  const double* aT;             // a^T (backward halves)
-  const double* ew;             // E, 626 x 8 iq: columns >= n zero, row 625 all ones
-  const double* emit;           // E, 625 x n (the backward half's first vector)
+  const double* aT;             // a^T (groups of backward halves)
+  const double* ef;             // E padded to er columns (zeros), row 625 = ones: 626 x er
+  const double* emit;           // E, 625 x n (a backward half's first vector)
   const double* init;           // pi E, 625 x n
   double* loglik;               // [plan blocks]
-  double* svec;                 // [slots x 2 x xr]
-  int* sK;                      // [slots x 2]
-  int prio_len;                 // tasks at least this long run at raised wave priority
+  double* svec;                 // split halves' vectors, row stride sstride
+  int64_t sstride;
+  int* sK;                      // their power-of-two exponents [slots x 2]
+  int prio_len;                 // groups at least this long run at raised wave priority
 };
-WaveVitGeometry wave_vit_geometry(int n);
-hipError_t launch_wave_fwd(const WaveVitGeometry& g, int grid, const WaveFwdArgs& p,
-                           hipStream_t st);
-hipError_t launch_wave_vit(const WaveVitGeometry& g, int grid, const VitArgs& p,
-                           hipStream_t st);
+struct WaveMfmaGeometry {
+  int cfg;      // configuration (negative: none for this n)
+  int block;    // threads per workgroup
+  int er;       // padded targets: width of the padded emission table
+  size_t lds;   // dynamic LDS bytes
+  int per_cu;   // resident workgroups per CU
+  bool mixed;   // the mixed launch (Viterbi blocks + forward groups, one queue) exists
+  size_t mixed_lds;
+  int mixed_per_cu;
+};
+WaveMfmaGeometry wave_mfma_geometry(int n);
+hipError_t launch_wave_mfma(const WaveMfmaGeometry& g, int grid, const WaveMfmaArgs& p,
+                            hipStream_t st);
+// forward groups and Viterbi blocks from one queue (wave_sweeps.hip): list entry e >= 0 = the
+// Viterbi block e (v), e < 0 = forward group -e - 1 (f); queue zero at launch
+hipError_t launch_wave_mixed(const WaveMfmaGeometry& g, int grid, const VitArgs& v,
+                             const WaveMfmaArgs& f, const int32_t* list, int nlist, int* queue,
+                             hipStream_t st);
 
 // log-likelihoods of the split blocks of a forward sweep
 hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,

@@ -49,6 +49,13 @@ static constexpr double LN2 = 0.69314718055994530942;
 // small device helpers
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// a wave-uniform 64-bit value into scalar registers (a per-lane copy of a uniform offset
+// makes every address built from it a 64-bit VGPR pair: register pressure and spills)
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -123,6 +130,27 @@ template <int QL>
 __device__ __forceinline__ double row_sum(double v) {
   if constexpr (QL == 4) v += dpp_f64<DPP_R4>(v);
   return v + dpp_f64<DPP_R8>(v);
+}
+
+// Stores through a wave-uniform base as a buffer resource (base and byte bound in SGPRs):
+// the per-lane part is one 32-bit byte offset instead of a 64-bit address pair, and a lane
+// whose offset is kOffNone (past the bound) stores nothing, without a branch.
+constexpr uint32_t kOffNone = 0xFFFFFFF0u;
+typedef unsigned int itr_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+// voff: the lane's byte offset (VGPR); soff: a wave-uniform byte offset (SGPR)
+__device__ __forceinline__ void buf_store_f64(__amdgpu_buffer_rsrc_t r, uint32_t voff,
+                                              uint32_t soff, double v) {
+  itr_u32x2 d;
+  d.x = (unsigned)__double2loint(v);
+  d.y = (unsigned)__double2hiint(v);
+  __builtin_amdgcn_raw_buffer_store_b64(d, r, voff, soff, 0);
+}
+__device__ __forceinline__ void buf_store_u16(__amdgpu_buffer_rsrc_t r, uint32_t voff,
+                                              uint32_t soff, uint16_t v) {
+  __builtin_amdgcn_raw_buffer_store_b16(v, r, voff, soff, 0);
 }
 
 // LDS hand-off between lanes of one wave (the region is private to the wave): a wave's LDS
