@@ -369,7 +369,7 @@ def main():
         if world > 1:
             dist.all_reduce(d_ll_global)
 
-    def opt_step(timing=False):
+    def opt_step(timing=False, xchg=True):
         # one objective evaluation at a nearby parameter vector (the simplex moves every
         # call): model rebuild on the device, forward log-likelihood of every block,
         # all-reduce of the per-block values (N > 1), host sum in block order
@@ -391,6 +391,8 @@ def main():
         hmm.forward_loglik_device(m1, plan, d_obs, out=d_ll)
         if timing:
             fwd_ms.append(hmm.last_kernel_ms("forward"))
+        if not xchg:
+            return 0.0
         exchange()
         acc = 0.0
         for y in d_ll_global.cpu().numpy().tolist():
@@ -398,9 +400,9 @@ def main():
         m1.close()
         return acc
 
-    def step(timing=False):
+    def step(timing=False, xchg=True):
         if opt_mode:
-            opt_step(timing)
+            opt_step(timing, xchg)
             return
         if post_mode:
             hmm.posterior_device(model, plan, d_obs, out=d_post)
@@ -414,13 +416,15 @@ def main():
             # returns when its outputs are complete, like the reference's wrappers (measured:
             # queueing the next step's fork/join behind the running one costs ~0.7 ms/step)
             hmm.forward_viterbi_device(model, plan, d_obs, out_ll=d_ll, out_path=d_path)
-            exchange()
+            if xchg:
+                exchange()
             torch.cuda.current_stream().synchronize()
             return
         hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
         if timing:
             fwd_ms.append(hmm.last_kernel_ms("forward"))
-        exchange()
+        if xchg:
+            exchange()
         hmm.viterbi_device(model, plan, d_obs, out=d_path)
         if timing:
             vit_ms.append(hmm.last_kernel_ms("viterbi"))
@@ -450,6 +454,31 @@ def main():
     for _ in range(max(1, min(args.steps, 3))):
         step(timing=True)
         torch.cuda.synchronize()
+    # N > 1: each rank's own step time without the exchange (its share of the work; the
+    # timed step waits for the slowest rank inside the all-reduce) and the exchange alone
+    per_rank_ms, xchg_ms = None, None
+    if world > 1:
+        own = []
+        for _ in range(max(1, min(args.steps, 3))):
+            torch.cuda.synchronize()
+            ts = time.perf_counter()
+            step(xchg=False)
+            torch.cuda.synchronize()
+            own.append((time.perf_counter() - ts) * 1e3)
+        ex = []
+        for _ in range(5):
+            dist.barrier()
+            torch.cuda.synchronize()
+            ts = time.perf_counter()
+            exchange()
+            torch.cuda.synchronize()
+            ex.append((time.perf_counter() - ts) * 1e3)
+        mine = torch.tensor([float(np.mean(own)), float(np.median(ex))], dtype=torch.float64,
+                            device=cdev)
+        allv = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        per_rank_ms = [round(float(v[0]), 3) for v in allv]
+        xchg_ms = round(max(float(v[1]) for v in allv), 4)
 
     ll_global = d_ll_global.cpu().numpy()
     acc = 0.0
@@ -601,6 +630,8 @@ def main():
                          "step_frac": round(ideal_ms / step_ms, 5) if not opt_mode else None},
             "cpu_baseline": cpu,
             **({"build_ms": round(float(np.mean(build_ms)), 1)} if opt_mode else {}),
+            **({"per_rank_step_ms": per_rank_ms, "allreduce_ms": xchg_ms,
+                "allreduce_bytes": int(d_ll_global.numel() * 8)} if world > 1 else {}),
             **({"host_path": host} if host is not None else {}),
             **(check or {}),
             "loglik_total": ll_total if args.mode != "posterior" else None,

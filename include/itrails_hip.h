@@ -201,6 +201,22 @@ ITR_API int itr_vanloan_paths(int n, const double* h_Q, int n_jobs, const double
                               int n_masks, const uint8_t* h_masks, int64_t n_paths,
                               const int32_t* h_path_job, const int64_t* h_path_off,
                               const int32_t* h_path_mask, double* d_out, void* stream);
+/* The same with the Pade branch input given: interval j's branch and scaling come from
+ * max(h_job_norm[j], the largest ||C_p t||_1 of the paths passed).  A rank-split model build
+ * evaluates a subset of an interval's paths on each rank; handing every rank the norms of the
+ * whole set (itr_vanloan_job_norms) makes each path's result identical to a single-rank
+ * evaluation.  h_job_norm may be null (= itr_vanloan_paths). */
+ITR_API int itr_vanloan_paths_ex(int n, const double* h_Q, int n_jobs, const double* h_t,
+                                 int n_masks, const uint8_t* h_masks, int64_t n_paths,
+                                 const int32_t* h_path_job, const int64_t* h_path_off,
+                                 const int32_t* h_path_mask, const double* h_job_norm,
+                                 double* d_out, void* stream);
+/* Host only: h_job_norm[j] = the largest ||C_p t_j||_1 over the paths of interval j (0 for
+ * an interval without paths), the quantity expm.py:16-143 chooses the Pade branch from. */
+ITR_API int itr_vanloan_job_norms(int n, const double* h_Q, int n_jobs, const double* h_t,
+                                  int n_masks, const uint8_t* h_masks, int64_t n_paths,
+                                  const int32_t* h_path_job, const int64_t* h_path_off,
+                                  const int32_t* h_path_mask, double* h_job_norm);
 
 /* Solve M_b X_b = R_b for b < batch (M n x n, R n x nrhs, row-major, contiguous batches).
  * M is overwritten by its LU factors (partial pivoting, first maximum |.| like LAPACK

@@ -1413,15 +1413,15 @@ int itr_expm_blocktri_batched(int n_block, int n_blocks, int64_t batch, const do
   return 0;
 }
 
-int itr_vanloan_paths(int n, const double* h_Q, int n_jobs, const double* h_t, int n_masks,
-                      const uint8_t* h_masks, int64_t n_paths, const int32_t* h_path_job,
-                      const int64_t* h_path_off, const int32_t* h_path_mask, double* d_out,
-                      void* stream) {
+namespace {
+int check_vanloan_paths(int n, const double* h_Q, int n_jobs, const double* h_t, int n_masks,
+                        const uint8_t* h_masks, int64_t n_paths, const int32_t* h_path_job,
+                        const int64_t* h_path_off, const int32_t* h_path_mask) {
   if (n < 1 || n_jobs < 0 || n_masks < 0 || n_paths < 0)
     return fail(ITR_EINVAL, "bad Van Loan shape n=%d jobs=%d masks=%d paths=%lld", n, n_jobs,
                 n_masks, (long long)n_paths);
   if (n_paths == 0) return 0;
-  if (!h_Q || !h_t || !h_path_job || !h_path_off || !h_path_mask || !d_out)
+  if (!h_Q || !h_t || !h_path_job || !h_path_off || !h_path_mask)
     return fail(ITR_EINVAL, "null pointer");
   if (h_path_off[0] != 0) return fail(ITR_EINVAL, "path offsets must start at 0");
   for (int64_t p = 0; p < n_paths; ++p) {
@@ -1437,12 +1437,51 @@ int itr_vanloan_paths(int n, const double* h_Q, int n_jobs, const double* h_t, i
                       h_path_mask[i]);
   }
   if (n_masks > 0 && !h_masks) return fail(ITR_EINVAL, "null masks");
+  return 0;
+}
+}  // namespace
+
+int itr_vanloan_paths_ex(int n, const double* h_Q, int n_jobs, const double* h_t, int n_masks,
+                         const uint8_t* h_masks, int64_t n_paths, const int32_t* h_path_job,
+                         const int64_t* h_path_off, const int32_t* h_path_mask,
+                         const double* h_job_norm, double* d_out, void* stream) {
+  if (int rc = check_vanloan_paths(n, h_Q, n_jobs, h_t, n_masks, h_masks, n_paths, h_path_job,
+                                   h_path_off, h_path_mask))
+    return rc;
+  if (n_paths == 0) return 0;
+  if (!d_out) return fail(ITR_EINVAL, "null pointer");
   hipStream_t st = (hipStream_t)stream;
   Scope sc("vanloan", st);
   const hipError_t e = itr::vanloan_paths(n, h_Q, n_jobs, h_t, n_masks, h_masks, n_paths,
-                                          h_path_job, h_path_off, h_path_mask, d_out, st);
+                                          h_path_job, h_path_off, h_path_mask, h_job_norm,
+                                          d_out, st);
   if (e != hipSuccess) return fail(ITR_EHIP, "Van Loan evaluation failed: %s",
                                    hipGetErrorString(e));
+  return 0;
+}
+
+int itr_vanloan_paths(int n, const double* h_Q, int n_jobs, const double* h_t, int n_masks,
+                      const uint8_t* h_masks, int64_t n_paths, const int32_t* h_path_job,
+                      const int64_t* h_path_off, const int32_t* h_path_mask, double* d_out,
+                      void* stream) {
+  return itr_vanloan_paths_ex(n, h_Q, n_jobs, h_t, n_masks, h_masks, n_paths, h_path_job,
+                              h_path_off, h_path_mask, nullptr, d_out, stream);
+}
+
+int itr_vanloan_job_norms(int n, const double* h_Q, int n_jobs, const double* h_t, int n_masks,
+                          const uint8_t* h_masks, int64_t n_paths, const int32_t* h_path_job,
+                          const int64_t* h_path_off, const int32_t* h_path_mask,
+                          double* h_job_norm) {
+  if (int rc = check_vanloan_paths(n, h_Q, n_jobs, h_t, n_masks, h_masks, n_paths, h_path_job,
+                                   h_path_off, h_path_mask))
+    return rc;
+  if (n_jobs > 0 && !h_job_norm) return fail(ITR_EINVAL, "null pointer");
+  if (n_paths == 0) {
+    for (int j = 0; j < n_jobs; ++j) h_job_norm[j] = 0.0;
+    return 0;
+  }
+  itr::vanloan_job_norms(n, h_Q, n_jobs, h_t, n_masks, h_masks, n_paths, h_path_job,
+                         h_path_off, h_path_mask, h_job_norm);
   return 0;
 }
 

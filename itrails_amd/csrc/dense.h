@@ -42,8 +42,12 @@ hipError_t expm_blocktri_batched(int nb, int kb, int64_t batch, const double* A,
 // arguments of itr_vanloan_paths)
 hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t, int nmasks,
                          const uint8_t* h_masks, int64_t npaths, const int32_t* h_job,
-                         const int64_t* h_off, const int32_t* h_mask, double* d_out,
-                         hipStream_t st);
+                         const int64_t* h_off, const int32_t* h_mask, const double* h_jnorm,
+                         double* d_out, hipStream_t st);
+// per interval, the largest ||C_p t||_1 over its paths (the Pade branch's input)
+void vanloan_job_norms(int nb, const double* h_Q, int njobs, const double* h_t, int nmasks,
+                       const uint8_t* h_masks, int64_t npaths, const int32_t* h_job,
+                       const int64_t* h_off, const int32_t* h_mask, double* jnorm);
 void release_vanloan_workspace();
 
 // emission rows (emission.hip): tables [n_states x 512] -> out [n_states x 256]

@@ -327,14 +327,9 @@ hipError_t ws_get(size_t dbytes, size_t hbytes, Ws** out) {
 
 void release_vanloan_workspace() { g_ws.release(); }
 
-hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t, int nmasks,
-                         const uint8_t* h_masks, int64_t npaths, const int32_t* h_job,
-                         const int64_t* h_off, const int32_t* h_mask, double* d_out,
-                         hipStream_t st) {
-  if (npaths <= 0) return hipSuccess;
-  const int64_t nn = (int64_t)nb * nb;
-
-  // ---- norms -> Pade branch and scaling per interval (expm.py:16-143) ----------------
+void vanloan_job_norms(int nb, const double* h_Q, int njobs, const double* h_t, int nmasks,
+                       const uint8_t* h_masks, int64_t npaths, const int32_t* h_job,
+                       const int64_t* h_off, const int32_t* h_mask, double* jnorm) {
   std::vector<double> cs(nb, 0.0);  // column sums of |Q|
   for (int r = 0; r < nb; ++r)
     for (int c = 0; c < nb; ++c) cs[c] += fabs(h_Q[(int64_t)r * nb + c]);
@@ -354,18 +349,37 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
     return best;
   };
   const double cmax = *std::max_element(cs.begin(), cs.end());
-  std::vector<double> jnorm(njobs, 0.0);
-  std::vector<char> jused(njobs, 0);
-  int maxlen = 1;
+  for (int j = 0; j < njobs; ++j) jnorm[j] = 0.0;
   for (int64_t p = 0; p < npaths; ++p) {
     const int j = h_job[p];
     const int L = (int)(h_off[p + 1] - h_off[p]);
-    maxlen = std::max(maxlen, L);
     double nm = cmax;
     for (int i = 1; i < L; ++i)
       nm = std::max(nm, pnorm(h_mask[h_off[p] + i - 1], h_mask[h_off[p] + i]));
     jnorm[j] = std::max(jnorm[j], nm * fabs(h_t[j]));
-    jused[j] = 1;
+  }
+}
+
+hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t, int nmasks,
+                         const uint8_t* h_masks, int64_t npaths, const int32_t* h_job,
+                         const int64_t* h_off, const int32_t* h_mask, const double* h_jnorm,
+                         double* d_out, hipStream_t st) {
+  if (npaths <= 0) return hipSuccess;
+  const int64_t nn = (int64_t)nb * nb;
+
+  // ---- norms -> Pade branch and scaling per interval (expm.py:16-143); a caller that
+  // evaluates a subset of an interval's paths (the rank-split build) passes the norms of the
+  // whole set so that every subset takes the same branch and scaling ----------------------
+  std::vector<double> jnorm(njobs, 0.0);
+  vanloan_job_norms(nb, h_Q, njobs, h_t, nmasks, h_masks, npaths, h_job, h_off, h_mask,
+                    jnorm.data());
+  if (h_jnorm)
+    for (int j = 0; j < njobs; ++j) jnorm[j] = std::max(jnorm[j], h_jnorm[j]);
+  std::vector<char> jused(njobs, 0);
+  int maxlen = 1;
+  for (int64_t p = 0; p < npaths; ++p) {
+    jused[h_job[p]] = 1;
+    maxlen = std::max(maxlen, (int)(h_off[p + 1] - h_off[p]));
   }
   std::vector<int> jm(njobs, 13), js(njobs, 0);
   for (int j = 0; j < njobs; ++j) branch_of(jnorm[j], &jm[j], &js[j]);

@@ -18,8 +18,8 @@ import numpy as np
 
 from ._lib import check, lib
 
-__all__ = ["expm", "expm_batched", "expm_blocktri_batched", "vanloan_paths", "solve_batched",
-           "gemm_batched"]
+__all__ = ["expm", "expm_batched", "expm_blocktri_batched", "vanloan_paths", "vanloan_job_norms",
+           "solve_batched", "gemm_batched"]
 
 
 def _dev(x):
@@ -64,13 +64,7 @@ def expm_blocktri_batched(A, n_blocks: int):
     return out if on_dev else out.cpu().numpy()
 
 
-def vanloan_paths(Q, t, masks_u8, path_job, path_off, path_mask):
-    """Van Loan integrals of many omega paths in one shared evaluation (itr_vanloan_paths):
-    returns a torch.cuda (n_paths, n, n) tensor, entry p = expm(C_p t[path_job[p]])[:n, -n:]
-    with C_p the block bidiagonal matrix of vanloan.py:392-425 for the mask ids
-    path_mask[path_off[p]:path_off[p+1]] (a length-1 path gives expm(Q t)).  Q, t, masks and
-    the path arrays are host NumPy arrays; nothing is synchronised."""
-    import torch
+def _vanloan_args(Q, t, masks_u8, path_job, path_off, path_mask):
     Q = np.ascontiguousarray(Q, dtype=np.float64)
     t = np.ascontiguousarray(t, dtype=np.float64)
     masks_u8 = np.ascontiguousarray(masks_u8, dtype=np.uint8)
@@ -81,15 +75,50 @@ def vanloan_paths(Q, t, masks_u8, path_job, path_off, path_mask):
     if Q.ndim != 2 or Q.shape[1] != n or masks_u8.ndim != 2 or \
             (masks_u8.size and masks_u8.shape[1] != n):
         raise ValueError("expected Q (n, n) and masks (n_masks, n)")
-    npaths = len(path_job)
-    if len(path_off) != npaths + 1:
+    if len(path_off) != len(path_job) + 1:
         raise ValueError("path_off must have n_paths + 1 entries")
+    return Q, t, masks_u8, path_job, path_off, path_mask
+
+
+def vanloan_paths(Q, t, masks_u8, path_job, path_off, path_mask, job_norm=None):
+    """Van Loan integrals of many omega paths in one shared evaluation (itr_vanloan_paths):
+    returns a torch.cuda (n_paths, n, n) tensor, entry p = expm(C_p t[path_job[p]])[:n, -n:]
+    with C_p the block bidiagonal matrix of vanloan.py:392-425 for the mask ids
+    path_mask[path_off[p]:path_off[p+1]] (a length-1 path gives expm(Q t)).  Q, t, masks and
+    the path arrays are host NumPy arrays; nothing is synchronised.  `job_norm` (per
+    interval, from vanloan_job_norms of a superset of the paths) fixes each interval's Pade
+    branch and scaling to that superset's (itr_vanloan_paths_ex)."""
+    import torch
+    Q, t, masks_u8, path_job, path_off, path_mask = _vanloan_args(
+        Q, t, masks_u8, path_job, path_off, path_mask)
+    n = Q.shape[0]
+    npaths = len(path_job)
     out = torch.empty((npaths, n, n), dtype=torch.float64, device="cuda")
     if npaths:
-        check(lib().itr_vanloan_paths(n, Q.ctypes.data, len(t), t.ctypes.data,
-                                      masks_u8.shape[0], masks_u8.ctypes.data, npaths,
+        jn = None
+        if job_norm is not None:
+            jn = np.ascontiguousarray(job_norm, dtype=np.float64)
+            if jn.shape != (len(t),):
+                raise ValueError("job_norm must have one entry per interval")
+        check(lib().itr_vanloan_paths_ex(n, Q.ctypes.data, len(t), t.ctypes.data,
+                                         masks_u8.shape[0], masks_u8.ctypes.data, npaths,
+                                         path_job.ctypes.data, path_off.ctypes.data,
+                                         path_mask.ctypes.data,
+                                         jn.ctypes.data if jn is not None else None,
+                                         out.data_ptr(), _stream()))
+    return out
+
+
+def vanloan_job_norms(Q, t, masks_u8, path_job, path_off, path_mask):
+    """Per interval, the largest ||C_p t||_1 of its paths (itr_vanloan_job_norms, host
+    only): the input of expm.py:16-143's Pade branch choice."""
+    Q, t, masks_u8, path_job, path_off, path_mask = _vanloan_args(
+        Q, t, masks_u8, path_job, path_off, path_mask)
+    out = np.zeros(len(t), dtype=np.float64)
+    check(lib().itr_vanloan_job_norms(Q.shape[0], Q.ctypes.data, len(t), t.ctypes.data,
+                                      masks_u8.shape[0], masks_u8.ctypes.data, len(path_job),
                                       path_job.ctypes.data, path_off.ctypes.data,
-                                      path_mask.ctypes.data, out.data_ptr(), _stream()))
+                                      path_mask.ctypes.data, out.ctypes.data))
     return out
 
 

@@ -561,60 +561,139 @@ def _group_matrices(S, steps, ng, n):
     return M
 
 
+def _unit_members(plan, tab, unit):
+    """The members (distinct (interval, sub-path) of length >= 2, vanloan.hip) a unit's paths
+    need; a propagator unit needs only its interval's root."""
+    i, g = unit
+    if g < 0:
+        return [((i,), 1)]
+    d = tab["ivs"][i]
+    off, pm = tab["off"], tab["pm"]
+    out = []
+    for pid in plan.intervals[i].groups[g][0]:
+        p = d.vl0 + int(pid)
+        w = tuple(int(x) for x in pm[off[p]:off[p + 1]])
+        for x in range(len(w)):
+            for y in range(x + 1, len(w)):
+                out.append(((i,) + w[x:y + 1], y + 1 - x))
+    return out
+
+
+def split_partition(plan, tab, world):
+    """Balanced partition of one rebuild's Van Loan work over `world` ranks.
+
+    Units are an interval's propagator expm(Q dt_i) and each of its path groups (the paths
+    one group matrix M_g = S_p0 + S_p1 + ... sums; groups share no path).  A rank's cost is
+    the distinct sub-paths ("members", vanloan.hip) its units need, each weighted by its
+    length (a member of length k is formed from k - 1 split products at every Pade step);
+    members shared by groups of one interval are formed once per rank that needs them.
+    Units go interval by interval (groups through the same inner omega pair adjacent) and
+    are cut into at most `world`
+    contiguous runs: the smallest per-rank cost bound T for which a greedy fill needs no more
+    than `world` runs (bisection on T).  Returns per rank (units, cost); unit = (interval,
+    -1 for the propagator or the group index)."""
+    off, pm = tab["off"], tab["pm"]
+
+    def first_path(i, g):
+        d = tab["ivs"][i]
+        return min(tuple(int(x) for x in pm[off[d.vl0 + int(p)]:off[d.vl0 + int(p) + 1]])
+                   for p in plan.intervals[i].groups[g][0])
+
+    units = []
+    for i, d in enumerate(tab["ivs"]):
+        units.append((i, -1))
+        # groups whose paths pass through the same inner omega pair share most members:
+        # keep them adjacent (at 8 ranks of the (7,7) chain: 1.23x instead of 1.33x the
+        # ideal per-rank cost)
+        fp = {g: first_path(i, g) for g in range(d.ng)}
+        units.extend((i, g) for g in sorted(range(d.ng), key=lambda g: (fp[g][1:3], fp[g])))
+    mem = [_unit_members(plan, tab, u) for u in units]
+
+    def fill(T):
+        runs, cur, seen, c = [], [], set(), 0.0
+        for u, ms in zip(units, mem):
+            inc = sum(w for k, w in set(ms) if k not in seen)
+            if cur and c + inc > T:
+                runs.append((cur, c))
+                cur, seen, c = [], set(), 0.0
+                inc = sum(w for k, w in set(ms))
+            cur.append(u)
+            seen.update(k for k, _ in ms)
+            c += inc
+        if cur:
+            runs.append((cur, c))
+        return runs
+
+    hi_runs = fill(float("inf"))
+    lo, hi = hi_runs[0][1] / max(world, 1), hi_runs[0][1]
+    best = hi_runs
+    for _ in range(40):
+        mid = 0.5 * (lo + hi)
+        runs = fill(mid)
+        if len(runs) <= world:
+            best, hi = runs, mid
+        else:
+            lo = mid
+    return best + [([], 0.0)] * (world - len(best))
+
+
 def _interval_mats_split(plan, tab, Q, t, la):
     """(E_i, M_i) of every interval with the Van Loan work divided over the ranks of
-    la.group: rank r evaluates intervals i = r, r + world, ... (their Van Loan paths and
-    propagators in one itr_vanloan_paths call) and their path-group sums; one all-gather of
-    [E_i, M_i] slots (zero-padded to the largest group count) shares them."""
+    la.group (split_partition: propagators and path groups cut into runs of equal member
+    cost).  Each rank evaluates its units' paths in one itr_vanloan_paths_ex call — every
+    interval's Pade branch and scaling taken from the norms of ALL its paths, so each path's
+    result is the single-rank one — and forms its group sums in path order; one all-gather
+    of the zero-padded unit slots shares them.  The result is bit-identical to world = 1."""
     import torch
     import torch.distributed as dist
     rank, world = la.rank, la.world
     n = Q.shape[0]
     ivs = tab["ivs"]
     I = len(ivs)
-    key = ("split", rank, world)
+    key = ("split", world)
     if key not in tab:
-        mine = [i for i in range(I) if i % world == rank]
-        job, off0, pm, loc = [], [0], [], []
-        for k, i in enumerate(mine):
-            d = ivs[i]
-            a, b = d.vl0, d.vl1
-            lo = len(job)
-            for p in range(a, b):
-                job.append(2 * k)
-                off0.append(off0[-1] + int(tab["off"][p + 1] - tab["off"][p]))
-                pm.extend(tab["pm"][tab["off"][p]:tab["off"][p + 1]].tolist())
-            e = len(job)
-            job.append(2 * k + 1)
-            off0.append(off0[-1] + 1)
-            pm.append(0)
-            loc.append((lo, e))
-        tab[key] = (mine, np.asarray(job, dtype=np.int32), np.asarray(off0, dtype=np.int64),
-                    np.asarray(pm, dtype=np.int32), loc)
-    mine, job, off0, pm, loc = tab[key]
-    slots = (I + world - 1) // world
-    gmax = max(d.ng for d in ivs)
-    buf = torch.zeros((slots, 1 + gmax, n, n), dtype=torch.float64, device=la.dev)
-    if mine:
-        tl = np.asarray([t[i] if j % 2 == 0 else t[I + i] for i in mine for j in (0, 1)],
-                        dtype=np.float64)
-        S = la.vanloan_batch(Q, tab["mask_u8"], tl, job, off0, pm)
-        for k, i in enumerate(mine):
-            d = ivs[i]
-            lo, e = loc[k]
-            buf[k, 0] = S[e]
-            if d.ng:
-                buf[k, 1:1 + d.ng] = _group_matrices(S[lo:e], d.sum_steps, d.ng, n)
+        parts = split_partition(plan, tab, world)
+        per_rank = []
+        for units, _ in parts:
+            job, off0, pm, steps = [], [0], [], []
+            for i, g in units:
+                d = ivs[i]
+                ps = [d.e_idx] if g < 0 else [d.vl0 + int(x) for x in plan.intervals[i].groups[g][0]]
+                loc = []
+                for p in ps:
+                    loc.append(len(job))
+                    job.append(int(tab["job"][p]))
+                    off0.append(off0[-1] + int(tab["off"][p + 1] - tab["off"][p]))
+                    pm.extend(tab["pm"][tab["off"][p]:tab["off"][p + 1]].tolist())
+                steps.append(loc)
+            per_rank.append((units, np.asarray(job, dtype=np.int32),
+                             np.asarray(off0, dtype=np.int64), np.asarray(pm, dtype=np.int32),
+                             _group_tables(la.dev, steps, [0] * len(steps))[0]))
+        tab[key] = ([c for _, c in parts], per_rank)
+    _, per_rank = tab[key]
+    units, job, off0, pm, steps = per_rank[rank]
+    slots = max(len(u[0]) for u in per_rank)
+    if units:
+        norms = la.vanloan_norms(Q, tab["mask_u8"], t, tab["job"], tab["off"], tab["pm"])
+        S = la.vanloan_batch(Q, tab["mask_u8"], t, job, off0, pm, job_norm=norms)
+        # slot k = M_g = S_p0 + S_p1 + ... in path order (a propagator: its S)
+        buf = _group_matrices(S, steps, slots, n)
+    else:
+        buf = torch.zeros((slots, n, n), dtype=torch.float64, device=la.dev)
     if buf.is_cuda and dist.get_backend(la.group) != "nccl":
         buf = buf.cpu()  # gloo rehearsal of the exchange (tests: ranks sharing one GPU)
     got = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(got, buf, group=la.group)
     got = [x.to(la.dev) for x in got]
-    out = []
-    for i, d in enumerate(ivs):
-        g = got[i % world][i // world]
-        out.append((g[0], g[1:1 + d.ng] if d.ng else None))
-    return out
+    E = [None] * I
+    M = [[None] * d.ng for d in ivs]
+    for r, pr in enumerate(per_rank):
+        for k, (i, g) in enumerate(pr[0]):
+            if g < 0:
+                E[i] = got[r][k]
+            else:
+                M[i][g] = got[r][k]
+    return [(E[i], torch.stack(M[i]) if ivs[i].ng else None) for i in range(I)]
 
 
 def _run_chain_abc_device(plan, Q, times, ss, probs: Dict, la) -> Dict:

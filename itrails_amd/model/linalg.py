@@ -23,9 +23,10 @@ _SPLIT_GROUP = [None]  # process group of a rank-split model build, see split_bu
 def split_build(enabled: bool = True, group=None):
     """Model builds started inside this context on a torch.distributed job divide their
     de-duplicated Van Loan work across the ranks of `group` (run_markov_chain_ABC.py:118-195
-    fans the reference's tasks out over processes the same way): interval i of the
-    three-species chain is evaluated by rank i mod world, which also forms its path-group
-    sums; one all-gather gives every rank all intervals' propagators and group matrices.
+    fans the reference's tasks out over processes the same way): the three-species chain's
+    propagators and path groups are cut into runs of equal Van Loan cost, one run per rank
+    (chains.split_partition), each rank forming its groups' sums; one all-gather gives every
+    rank all intervals' propagators and group matrices, bit-identical to a one-rank build.
     Every rank of the group must build the same model at the same time (the optimizer's
     objective evaluations do)."""
     prev = _SPLIT_GROUP[0]
@@ -95,12 +96,20 @@ class DeviceLinalg:
 
     # ---- device-resident forms (torch.cuda tensors out; used by the planned chains) -----
     def vanloan_batch(self, Q: np.ndarray, masks_u8: np.ndarray, t: np.ndarray,
-                      path_job: np.ndarray, path_off: np.ndarray, path_mask: np.ndarray):
+                      path_job: np.ndarray, path_off: np.ndarray, path_mask: np.ndarray,
+                      job_norm=None):
         """(n_paths, n, n) device tensor of Van Loan integrals over several intervals at once
-        (dense.vanloan_paths: shared sub-path evaluation, vanloan.hip)."""
+        (dense.vanloan_paths: shared sub-path evaluation, vanloan.hip); `job_norm` fixes the
+        intervals' Pade branches (vanloan_norms of a superset of the paths)."""
         from ..dense import vanloan_paths
         self.stats["vanloan"] += len(path_job)
-        return vanloan_paths(Q, t, masks_u8, path_job, path_off, path_mask)
+        return vanloan_paths(Q, t, masks_u8, path_job, path_off, path_mask, job_norm)
+
+    def vanloan_norms(self, Q: np.ndarray, masks_u8: np.ndarray, t: np.ndarray,
+                      path_job: np.ndarray, path_off: np.ndarray, path_mask: np.ndarray):
+        """Per interval, the largest ||C_p t||_1 of its paths (host only)."""
+        from ..dense import vanloan_job_norms
+        return vanloan_job_norms(Q, t, masks_u8, path_job, path_off, path_mask)
 
     def deepest_t(self, Q: np.ndarray, masks: Dict[Omega, np.ndarray],
                   paths: Sequence[Tuple[Omega, ...]]):

@@ -52,7 +52,7 @@ class FakeTorchLinalg(FakeNumpyLinalg):
     dev = torch.device("cpu")
     rank, world, group = 0, 1, None
 
-    def vanloan_batch(self, Q, masks_u8, t, path_job, path_off, path_mask):
+    def vanloan_batch(self, Q, masks_u8, t, path_job, path_off, path_mask, job_norm=None):
         n = Q.shape[0]
         out = []
         for p in range(len(path_job)):
@@ -63,6 +63,9 @@ class FakeTorchLinalg(FakeNumpyLinalg):
         self.stats["vanloan"] += len(path_job)
         return torch.from_numpy(np.stack(out)) if out else torch.zeros((0, n, n),
                                                                        dtype=torch.float64)
+
+    def vanloan_norms(self, Q, masks_u8, t, path_job, path_off, path_mask):
+        return np.zeros(len(t))
 
     def deepest_t(self, Q, masks, paths):
         n = Q.shape[0]

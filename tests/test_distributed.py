@@ -145,17 +145,26 @@ def _split_build_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_split_model_build_gloo_matches_single_rank(world):
-    """The rank-split model build (chains._interval_mats_split: interval i's Van Loan
-    paths, propagator and group sums on rank i mod world, one all-gather) gives every rank
-    the single-rank model; each rank evaluates only its own intervals' paths."""
+    """The rank-split model build (chains._interval_mats_split: propagators and path groups
+    cut into runs of equal Van Loan member cost, one run per rank, one all-gather) gives
+    every rank the single-rank model bit for bit; each path is evaluated on exactly one rank
+    and every rank's member cost is within 1.3x of the mean."""
     import torch.multiprocessing as mp
     from helpers.torch_linalg import FakeTorchLinalg
-    from itrails_amd.model import trans_emiss_calc
+    from itrails_amd.model import chains, trans_emiss_calc
     g = golden("model_kat_3_3.npz")
     la = FakeTorchLinalg()
     a1, _, pi1, _, _ = trans_emiss_calc(*g["args"], 3, 3, la=la)
+    plan = chains._LAST_PLAN[3]
+    (tab,) = plan.dev.values()
+    parts = chains.split_partition(plan, tab, world)
+    costs = np.array([c for _, c in parts])
+    assert costs.max() <= 1.3 * costs.mean(), costs
+    units = [u for pu, _ in parts for u in pu]
+    assert sorted(units) == sorted(set(units)) and len(units) == sum(
+        1 + len(ip.groups) for ip in plan.intervals)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -170,3 +179,22 @@ def test_split_model_build_gloo_matches_single_rank(world):
     for _, a, pi, _ in res:
         assert np.array_equal(a, a1) and np.array_equal(pi, pi1)
     assert sum(v for _, _, _, v in res) == la.stats["vanloan"]
+
+
+def test_split_partition_balanced_at_7_intervals():
+    """Config 5's (7,7) chain plan over 2..8 ranks: every rank's member cost within 1.3x of
+    the mean (the old interval-mod-world split left 2 of 8 ranks idle)."""
+    from helpers.torch_linalg import FakeTorchLinalg
+    from itrails_amd.model import chains, trans_emiss_calc
+    g = golden("model_kat_3_3.npz")
+    la = FakeTorchLinalg()
+    trans_emiss_calc(*g["args"], 7, 7, la=la)
+    plan = chains._LAST_PLAN[7]
+    (tab,) = plan.dev.values()
+    for world in (2, 4, 8):
+        costs = np.array([c for _, c in chains.split_partition(plan, tab, world)])
+        assert costs.max() <= 1.3 * costs.mean(), (world, costs)
+        # members shared by groups on two ranks are formed twice: the largest rank's cost
+        # stays within 1.25x of an even split of the one-rank work
+        one = chains.split_partition(plan, tab, 1)[0][1]
+        assert costs.max() <= 1.25 * one / world, (world, costs, one)

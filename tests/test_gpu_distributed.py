@@ -120,11 +120,13 @@ def _split_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_split_model_build_two_ranks_matches_single_rank(gpu):
-    """The rank-split (5,5) model build on the real HIP path (two gloo ranks on cuda:0):
-    each rank evaluates half of the intervals' Van Loan paths, the all-gather shares them,
-    and every rank's model equals the single-rank build bit for bit (and the reference's
-    within the model tolerance)."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_split_model_build_ranks_match_single_rank(gpu, world):
+    """The rank-split (5,5) model build on the real HIP path (gloo ranks on cuda:0): each
+    rank evaluates its run of the propagators and path groups (chains.split_partition;
+    intervals cut mid-way, each interval's Pade branch fixed by the norms of all its paths),
+    the all-gather shares them, and every rank's model equals the single-rank build bit for
+    bit (and the reference's within the model tolerance)."""
     import torch.multiprocessing as mp
     from itrails_amd.model import trans_emiss_calc
     from itrails_amd.model.linalg import DeviceLinalg
@@ -134,7 +136,7 @@ def test_split_model_build_two_ranks_matches_single_rank(gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_split_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
