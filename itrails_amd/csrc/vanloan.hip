@@ -7,16 +7,29 @@
 // top-right block.  Every polynomial of a block upper triangular matrix, the Pade quotient and
 // its squarings are block upper triangular again, and block (i, j) of any of them depends
 // only on the sub-path w_i .. w_j.  So block (0, k-1) of every intermediate is a function of
-// a distinct sub-path ("member"): the diagonal block Q t is one member per interval, each
-// consecutive omega pair another, and so on.  One rebuild of the (5,5) model asks for ~1400
-// paths of length <= 5 over four intervals; they share ~500 distinct sub-paths per interval,
-// so the evaluation here forms ~3.8x fewer block products than path-by-path expm, with no
-// (L n)^2 matrices at all.
+// a distinct sub-path ("member"): the diagonal block Q t is one member per interval ("root"),
+// each consecutive omega pair another, and so on.  One rebuild of the (5,5) model asks for
+// ~1400 paths of length <= 5 over four intervals; they share ~500 distinct sub-paths per
+// interval, so the evaluation here forms ~3.8x fewer block products than path-by-path expm,
+// with no (L n)^2 matrices at all.
+//
+// Supports.  Block (0, k-1) of any product of C's blocks is a sum of chains
+// Q^a D_{w0} Q D_{w1} Q^b ... Q^z (D_w = diag(m_w)): row r can be non-zero only if r reaches a
+// state of class w_0 in Q's transition graph, column c only if c is reached from class
+// w_{k-1}.  The coalescent CTMCs are nearly acyclic (reach density ~0.3) and the classes
+// small, so a non-root member of the (5,5) rebuild lives on ~44 rows x ~5 columns of 203 x 203,
+// and the inner index of a split X[s_0..l] Y[s_l..] runs only over the states both reached
+// from and reaching class w_l.  Non-root members are stored compactly (their support rectangle,
+// row-major); every other entry of the reference's dense evaluation is an exact zero (sums of
+// products with a zero factor), so dropping them changes nothing but the order in which the
+// non-zero terms are added.  Roots stay dense (n x n).
 //
 //   product  Z = alpha X Y + beta D + gamma I:  Z[s] = sum_l X[s_0..l] Y[s_l..k-1] over the
-//            splits of member s (pair_gemm_kernel: one 64x64 output tile per workgroup,
-//            v_mfma_f64_16x16x4, the K loop running across the member's split pairs; members
-//            of zero blocks — e.g. sub-paths longer than 3 of A^2 — are never read)
+//            splits of member s.  Roots: pair_gemm_kernel (one 64x64 output tile per
+//            workgroup, v_mfma_f64_16x16x4, the K loop running across split pairs).  Compact
+//            members: compact_gemm_kernel (one workgroup per ~256 output entries, K lists of
+//            the split's support intersection).  Members of zero blocks — e.g. sub-paths longer
+//            than 3 of A^2 — are never read.
 //   solve    (V - U) R = V + U by block back substitution: the one diagonal block of each
 //            interval inverted by LU (dense.hip), then by sub-path length
 //            R[s] = inv (N[s] - sum_{l>=1} M[s_0..l] R[s_l..k-1])
@@ -42,25 +55,25 @@ namespace {
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 constexpr int TT = 64, TK = 16;
-constexpr int IDENT = 1 << 30;  // output member flag: add gamma I
 
 struct PairGemmArgs {
   int nb;        // block order
   int tn;        // tiles per block row (ceil(nb / 64))
-  int64_t nout;  // output members in this launch
+  int64_t nout;  // output roots in this launch
   const double* X;
   const double* Y;
   double* Z;
   const double* D;  // may alias Z (read before written, same thread)
   double alpha, beta, gamma;
-  const int* out;   // [nout] output member (| IDENT)
+  const int* zoff;  // [nout] output offset (doubles) in Z and D
+  const int* zid;   // [nout] 1: add gamma I
   const int* pofs;  // [nout + 1] split-pair range
-  const int* px;    // X member of each pair
-  const int* py;    // Y member of each pair
+  const int* px;    // X offset (doubles) of each pair
+  const int* py;    // Y offset of each pair
 };
 
-// One 64x64 tile of one output member.  The grid is a multiple of 8 and workgroup b runs on
-// XCD b % 8: logical tile ids are dealt so that the tiles of one member (which read the same
+// One 64x64 tile of one dense (root) output.  The grid is a multiple of 8 and workgroup b runs
+// on XCD b % 8: logical tile ids are dealt so that the tiles of one output (which read the same
 // X and Y blocks) land on the same XCD and share its L2.
 __global__ void __launch_bounds__(256) pair_gemm_kernel(PairGemmArgs g) {
   // A tile kept row-major (m, k) with a pitch of 17 doubles and the B tile (k, n) with a
@@ -78,9 +91,6 @@ __global__ void __launch_bounds__(256) pair_gemm_kernel(PairGemmArgs g) {
   const int tile = (int)(logical - oi * tiles);
   const int tm = tile / g.tn, tnn = tile - tm * g.tn;
   const int nb = g.nb;
-  const int64_t nn = (int64_t)nb * nb;
-  const int ow = g.out[oi];
-  const int o = ow & (IDENT - 1);
   const int p0 = g.pofs[oi], p1 = g.pofs[oi + 1];
   const int ksteps = (nb + TK - 1) / TK;
   const int nsteps = (p1 - p0) * ksteps;
@@ -110,8 +120,8 @@ __global__ void __launch_bounds__(256) pair_gemm_kernel(PairGemmArgs g) {
   auto fetch = [&](int step) {
     const int pr = p0 + step / ksteps;
     const int k0 = (step % ksteps) * TK;
-    const double* __restrict__ A = g.X + (int64_t)g.px[pr] * nn;
-    const double* __restrict__ B = g.Y + (int64_t)g.py[pr] * nn;
+    const double* __restrict__ A = g.X + g.px[pr];
+    const double* __restrict__ B = g.Y + g.py[pr];
     const int gr = row0 + ar;
 #pragma unroll
     for (int h = 0; h < RA; ++h)
@@ -154,9 +164,10 @@ __global__ void __launch_bounds__(256) pair_gemm_kernel(PairGemmArgs g) {
     __syncthreads();
   }
 
-  double* __restrict__ C = g.Z + (int64_t)o * nn;
-  const double* Dm = g.D ? g.D + (int64_t)o * nn : nullptr;
-  const double gam = (ow & IDENT) ? g.gamma : 0.0;
+  const int zo = g.zoff[oi];
+  double* __restrict__ C = g.Z + zo;
+  const double* Dm = g.D ? g.D + zo : nullptr;
+  const double gam = g.zid[oi] ? g.gamma : 0.0;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -174,11 +185,62 @@ __global__ void __launch_bounds__(256) pair_gemm_kernel(PairGemmArgs g) {
       }
 }
 
-// out[m] = sum_t c[t] in[t][m] + (m < nident ? cI I : 0) over members [0, count)
+// Compact outputs: Z[s][i][j] = alpha sum_pairs sum_t X[xrow_i + kx_t] Y[ycol_j + ky_t ldy]
+// + beta D[s][i][j] on the member's support rectangle (R x C, row-major).  X rows: a root
+// (dense, the member's row states) or a compact member with the same row set; Y columns
+// likewise.  Work item = a run of rows of one output (about 256 entries).
+constexpr int kOH = 7;  // output header: zoff, R, C, rows_at, cols_at, pair begin, pair end
+constexpr int kPH = 8;  // pair header: xoff, ldx, xroot, yoff, ldy, yroot, k_at, klen
+struct CompactArgs {
+  int nb;
+  int nitems;
+  const int* items;  // [nitems][3]: output, first row, rows
+  const int* ohdr;
+  const int* phdr;
+  const int* tab;    // state lists and K lists (kx[klen] then ky[klen])
+  const double* X;
+  const double* Y;
+  double* Z;
+  const double* D;
+  double alpha, beta;
+};
+
+__global__ void __launch_bounds__(256) compact_gemm_kernel(CompactArgs a) {
+  const int it = blockIdx.x;
+  if (it >= a.nitems) return;
+  const int o = a.items[3 * it], row0 = a.items[3 * it + 1], nrows = a.items[3 * it + 2];
+  const int* oh = a.ohdr + kOH * o;
+  const int zoff = oh[0], C = oh[2];
+  const int* rows = a.tab + oh[3];
+  const int* cols = a.tab + oh[4];
+  const int pb = oh[5], pe = oh[6];
+  for (int e = threadIdx.x; e < nrows * C; e += 256) {
+    const int ri = e / C;
+    const int i = row0 + ri, jj = e - ri * C;
+    double acc = 0.0;
+    for (int q = pb; q < pe; ++q) {
+      const int* ph = a.phdr + kPH * q;
+      const double* xr = a.X + ph[0] + (ph[2] ? (int64_t)rows[i] * a.nb : (int64_t)i * ph[1]);
+      const double* yc = a.Y + ph[3] + (ph[5] ? cols[jj] : jj);
+      const int ldy = ph[4];
+      const int klen = ph[7];
+      const int* kx = a.tab + ph[6];
+      const int* ky = kx + klen;
+      for (int t = 0; t < klen; ++t) acc = fma(xr[kx[t]], yc[(int64_t)ky[t] * ldy], acc);
+    }
+    const int64_t zi = zoff + (int64_t)i * C + jj;
+    double v = a.alpha * acc;
+    if (a.D) v += a.beta * a.D[zi];
+    a.Z[zi] = v;
+  }
+}
+
+// out[e] = sum_t c[t] in[t][e] + (e in a root's diagonal ? cI : 0) over one member range
+// (roots first: nident elements = the range's roots, n x n each)
 struct LinArgs {
   int nb;
-  int64_t count;
-  int64_t nident;
+  int64_t count;   // elements
+  int64_t nident;  // elements of the leading roots
   double* out;
   const double* in[4];
   double c[4];
@@ -187,59 +249,84 @@ struct LinArgs {
 
 __global__ void __launch_bounds__(256) member_lincomb_kernel(LinArgs a) {
   const int64_t nn = (int64_t)a.nb * a.nb;
-  const int64_t total = a.count * nn;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < a.count;
        e += (int64_t)gridDim.x * 256) {
     double v = 0.0;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
       if (a.in[t]) v += a.c[t] * a.in[t][e];
-    const int64_t m = e / nn, r = (e - m * nn) / a.nb, c = e - m * nn - r * a.nb;
-    if (m < a.nident && r == c) v += a.cI;
+    if (e < a.nident) {
+      const int64_t w = e % nn;
+      if (w / a.nb == w % a.nb) v += a.cI;
+    }
     a.out[e] = v;
   }
 }
 
-// A of every member: roots Q t_j 2^-s_j, consecutive pairs diag(m_a) Q diag(m_b) t_j 2^-s_j
-// (the reference's C t / 2^s: (q t) then the exact power of two), longer sub-paths 0
+// A of every member: roots Q t_j 2^-s_j (dense), consecutive pairs diag(m_a) Q diag(m_b) t_j
+// 2^-s_j on their support rectangle (the reference's C t / 2^s: (q t) then the exact power of
+// two), longer sub-paths 0
+constexpr int kMD = 8;  // member descriptor: kind, mask a, mask b, offset, R, C, rows_at, cols_at
 struct BuildArgs {
   int nb;
-  int64_t count;
   const double* Q;      // nb x nb
   const double* masks;  // [nmasks][nb] 0/1
-  const int* desc;      // [count][3]: kind (0 root, 1 pair, 2 zero), mask a, mask b
+  const int* desc;      // [count][kMD]
+  const int* tab;
   const double* tau;    // [count][2]: t_j, 2^-s_j
   double* A;
 };
 
 __global__ void __launch_bounds__(256) build_members_kernel(BuildArgs a) {
   const int64_t m = blockIdx.y;
-  const int kind = a.desc[3 * m];
-  const double* ma = a.masks + (int64_t)a.desc[3 * m + 1] * a.nb;
-  const double* mb = a.masks + (int64_t)a.desc[3 * m + 2] * a.nb;
+  const int* d = a.desc + kMD * m;
+  const int kind = d[0];
+  const double* ma = a.masks + (int64_t)d[1] * a.nb;
+  const double* mb = a.masks + (int64_t)d[2] * a.nb;
   const double t = a.tau[2 * m], sc = a.tau[2 * m + 1];
-  const int64_t nn = (int64_t)a.nb * a.nb;
-  double* out = a.A + m * nn;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nn;
+  const int64_t size = kind == 0 ? (int64_t)a.nb * a.nb : (int64_t)d[4] * d[5];
+  const int C = d[5];
+  const int* rows = a.tab + d[6];
+  const int* cols = a.tab + d[7];
+  double* out = a.A + d[3];
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < size;
        e += (int64_t)gridDim.x * 256) {
-    const int r = (int)(e / a.nb), c = (int)(e - (int64_t)r * a.nb);
     double v = 0.0;
-    if (kind == 0) v = (a.Q[e] * t) * sc;
-    else if (kind == 1) v = ((ma[r] * a.Q[e] * mb[c]) * t) * sc;
+    if (kind == 0) {
+      v = (a.Q[e] * t) * sc;
+    } else if (kind == 1) {
+      const int i = (int)(e / C), j = (int)(e - (int64_t)i * C);
+      const int r = rows[i], c = cols[j];
+      v = ((ma[r] * a.Q[(int64_t)r * a.nb + c] * mb[c]) * t) * sc;
+    }
     out[e] = v;
   }
 }
 
-// out[i] = src[sel[i]][idx[i]]  (two candidate buffers)
-__global__ void __launch_bounds__(256) gather_members_kernel(int nb, const double* s0,
-                                                             const double* s1, const int* idx,
-                                                             const int* sel, double* out) {
-  const int64_t i = blockIdx.y;
+// out[p] (dense n x n) = path p's member, scattered from its support rectangle
+constexpr int kPD = 6;  // path descriptor: offset, C, root, rowpos_at, colpos_at, buffer
+__global__ void __launch_bounds__(256) scatter_paths_kernel(int nb, const double* s0,
+                                                            const double* s1, const int* pdesc,
+                                                            const int* tab, double* out) {
+  const int64_t p = blockIdx.y;
   const int64_t nn = (int64_t)nb * nb;
-  const double* s = (sel[i] ? s1 : s0) + (int64_t)idx[i] * nn;
+  const int* d = pdesc + kPD * p;
+  const double* s = (d[5] ? s1 : s0) + d[0];
+  const int C = d[1];
+  const int* rp = tab + d[3];
+  const int* cp = tab + d[4];
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nn;
-       e += (int64_t)gridDim.x * 256)
-    out[i * nn + e] = s[e];
+       e += (int64_t)gridDim.x * 256) {
+    double v;
+    if (d[2]) {
+      v = s[e];
+    } else {
+      const int r = (int)(e / nb), c = (int)(e - (int64_t)r * nb);
+      const int i = rp[r], j = cp[c];
+      v = (i >= 0 && j >= 0) ? s[(int64_t)i * C + j] : 0.0;
+    }
+    out[p * nn + e] = v;
+  }
 }
 
 // Pade coefficients (expm.py:29-140; same values as dense.hip)
@@ -375,14 +462,71 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
                     jnorm.data());
   if (h_jnorm)
     for (int j = 0; j < njobs; ++j) jnorm[j] = std::max(jnorm[j], h_jnorm[j]);
-  std::vector<char> jused(njobs, 0);
   int maxlen = 1;
-  for (int64_t p = 0; p < npaths; ++p) {
-    jused[h_job[p]] = 1;
-    maxlen = std::max(maxlen, (int)(h_off[p + 1] - h_off[p]));
-  }
+  for (int64_t p = 0; p < npaths; ++p) maxlen = std::max(maxlen, (int)(h_off[p + 1] - h_off[p]));
   std::vector<int> jm(njobs, 13), js(njobs, 0);
   for (int j = 0; j < njobs; ++j) branch_of(jnorm[j], &jm[j], &js[j]);
+
+  // ---- supports: transitive closure of Q's transition graph (bit rows, Warshall) ---------
+  const int NW = (nb + 63) / 64;
+  std::vector<uint64_t> reach((size_t)nb * NW, 0);
+  auto bit = [&](int r, int c) { return (reach[(size_t)r * NW + (c >> 6)] >> (c & 63)) & 1; };
+  for (int r = 0; r < nb; ++r) {
+    reach[(size_t)r * NW + (r >> 6)] |= 1ull << (r & 63);
+    for (int c = 0; c < nb; ++c)
+      if (h_Q[(int64_t)r * nb + c] != 0.0) reach[(size_t)r * NW + (c >> 6)] |= 1ull << (c & 63);
+  }
+  for (int k = 0; k < nb; ++k)
+    for (int i = 0; i < nb; ++i)
+      if (bit(i, k))
+        for (int w = 0; w < NW; ++w) reach[(size_t)i * NW + w] |= reach[(size_t)k * NW + w];
+  // per class w: rows reaching it (to) and columns reached from it (from), as state lists,
+  // position maps and the K lists of the splits (ints of one table, `T`)
+  std::vector<int> T;
+  T.reserve(1 << 16);
+  const int iota_at = 0;
+  for (int i = 0; i < nb; ++i) T.push_back(i);
+  std::vector<int> to_n(nmasks), fr_n(nmasks), rl_at(nmasks), rr_at(nmasks), md_at(nmasks),
+      md_n(nmasks), rp_at(nmasks), cp_at(nmasks);
+  for (int w = 0; w < nmasks; ++w) {
+    const uint8_t* mw = h_masks + (int64_t)w * nb;
+    std::vector<uint64_t> fr(NW, 0);
+    std::vector<int> tl, fl;
+    for (int m = 0; m < nb; ++m)
+      if (mw[m])
+        for (int x = 0; x < NW; ++x) fr[x] |= reach[(size_t)m * NW + x];
+    for (int r = 0; r < nb; ++r) {
+      bool hit = false;
+      for (int m = 0; m < nb && !hit; ++m) hit = mw[m] && bit(r, m);
+      if (hit) tl.push_back(r);
+      if ((fr[r >> 6] >> (r & 63)) & 1) fl.push_back(r);
+    }
+    to_n[w] = (int)tl.size();
+    fr_n[w] = (int)fl.size();
+    rl_at[w] = (int)T.size();  // to-states, then 0 .. R-1
+    T.insert(T.end(), tl.begin(), tl.end());
+    for (int i = 0; i < to_n[w]; ++i) T.push_back(i);
+    rr_at[w] = (int)T.size();  // 0 .. C-1, then from-states
+    for (int i = 0; i < fr_n[w]; ++i) T.push_back(i);
+    T.insert(T.end(), fl.begin(), fl.end());
+    std::vector<int> tp(nb, -1), fp(nb, -1);
+    for (int i = 0; i < to_n[w]; ++i) tp[tl[i]] = i;
+    for (int i = 0; i < fr_n[w]; ++i) fp[fl[i]] = i;
+    std::vector<int> kx, ky;  // K = from(w) & to(w): X column / Y row positions
+    for (int s = 0; s < nb; ++s)
+      if (fp[s] >= 0 && tp[s] >= 0) {
+        kx.push_back(fp[s]);
+        ky.push_back(tp[s]);
+      }
+    md_at[w] = (int)T.size();
+    md_n[w] = (int)kx.size();
+    T.insert(T.end(), kx.begin(), kx.end());
+    T.insert(T.end(), ky.begin(), ky.end());
+    rp_at[w] = (int)T.size();
+    T.insert(T.end(), tp.begin(), tp.end());
+    cp_at[w] = (int)T.size();
+    T.insert(T.end(), fp.begin(), fp.end());
+  }
 
   // ---- members: distinct (interval, sub-path); roots carry an empty sequence -------------
   typedef std::pair<int, std::vector<int>> Key;
@@ -420,6 +564,21 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
     if (a == b) return root_of(k.first);
     return id.at(Key{k.first, std::vector<int>(k.second.begin() + a, k.second.begin() + b + 1)});
   };
+  // support rectangle and offset (doubles) of every member, the same in every work buffer
+  std::vector<int> mR(NM), mC(NM), moff(NM + 1);
+  int64_t tot = 0;
+  for (int i = 0; i < NM; ++i) {
+    if (mlen(mem[i]) == 1) {
+      mR[i] = mC[i] = nb;
+    } else {
+      mR[i] = to_n[mem[i].second.front()];
+      mC[i] = fr_n[mem[i].second.back()];
+    }
+    moff[i] = (int)tot;
+    tot += (int64_t)mR[i] * mC[i];
+    if (tot >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  }
+  moff[NM] = (int)tot;
   // splits l = 0 .. k-1 of each member: (X member s_0..l, Y member s_l..k-1)
   std::vector<std::vector<std::pair<int, int>>> splits(NM);
   for (int i = 0; i < NM; ++i) {
@@ -431,8 +590,7 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
     for (int l = 0; l < L; ++l) splits[i].push_back({sub(mem[i], 0, l), sub(mem[i], l, L - 1)});
   }
 
-  // ---- workspace: 8 member buffers, inverses, Q, masks, descriptors ----------------------
-  const int64_t W = (int64_t)NM * nn;
+  // ---- launch plan -----------------------------------------------------------------------
   std::vector<int> groups_m;  // distinct branches in member order
   std::vector<int> gbeg, gend;
   for (int i = 0; i < NM; ++i) {
@@ -444,54 +602,156 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
     }
     gend.back() = i + 1;
   }
-  // host descriptor stream (ints), doubles after it
-  std::vector<int> H;
-  H.reserve(1 << 16);
+  // host descriptor stream (ints): the support table first, doubles after the ints
+  std::vector<int> H(T);
+  H.reserve(T.size() + (1 << 16));
   auto put = [&](int v) {
     H.push_back(v);
     return (int64_t)H.size() - 1;
   };
   struct Launch {
-    int kind;  // 0 pair gemm, 1 lincomb, 2 solve roots, 3 gather out
-    int x, y, z, d;  // buffer ids (-1 none); 8 = inverse buffer
+    int kind;  // 0 dense root product, 1 lincomb, 2 invert roots, 4 compact product
+    int x, y, z, d;  // buffer ids (-1 none); NINV = the root inverses
     double alpha, beta, gamma;
-    int64_t out_at, pofs_at, px_at, py_at;
-    int64_t nout;
+    int64_t a0, a1, a2, a3, a4;  // descriptor offsets in H
+    int64_t n0;                  // outputs / work items
   };
   std::vector<Launch> L;
   int nz[9];
   const int NINV = 8;
-  // product over members of [g0, g1): Z = alpha X Y + beta D + gamma I
+  // one split pair of compact output s: X = member a (or the inverse slot `inv`), Y = member b
+  auto pair_hdr = [&](int s, int a, int b, int l, int inv) {
+    const std::vector<int>& seq = mem[s].second;
+    const bool xroot = inv >= 0 || mlen(mem[a]) == 1, yroot = mlen(mem[b]) == 1;
+    int k_at, klen;
+    if (xroot) {  // K = rows of s: root columns = states, Y rows = positions
+      k_at = rl_at[seq.front()];
+      klen = to_n[seq.front()];
+    } else if (yroot) {  // K = columns of s: X columns = positions, root rows = states
+      k_at = rr_at[seq.back()];
+      klen = fr_n[seq.back()];
+    } else {  // K = states both reached from and reaching class seq[l]
+      k_at = md_at[seq[l]];
+      klen = md_n[seq[l]];
+    }
+    put(inv >= 0 ? (int)(inv * nn) : moff[a]);
+    put(xroot ? nb : mC[a]);
+    put(xroot ? 1 : 0);
+    put(moff[b]);
+    put(yroot ? nb : mC[b]);
+    put(yroot ? 1 : 0);
+    put(k_at);
+    put(klen);
+  };
+  // compact launch over outputs `outs` with pair lists `pl` (pair index l per entry)
+  auto compact_launch = [&](int X, int Y, int Z, int D, double alpha, double beta,
+                            const std::vector<int>& outs,
+                            const std::vector<std::vector<std::pair<int, int>>>& pl,
+                            const std::vector<std::vector<int>>& pls, int inv_g0) {
+    if (outs.empty()) return;
+    Launch ln{4, X, Y, Z, D, alpha, beta, 0.0, 0, 0, 0, 0, 0, 0};
+    ln.a2 = (int64_t)H.size();  // pair headers
+    std::vector<int> pbeg(outs.size()), pend(outs.size());
+    int np = 0;
+    for (size_t q = 0; q < outs.size(); ++q) {
+      pbeg[q] = np;
+      for (size_t t = 0; t < pl[q].size(); ++t) {
+        const int a = pl[q][t].first, b = pl[q][t].second;
+        pair_hdr(outs[q], a, b, pls[q][t], inv_g0 >= 0 ? root_of(mem[outs[q]].first) - inv_g0 : -1);
+        ++np;
+      }
+      pend[q] = np;
+    }
+    ln.a1 = (int64_t)H.size();  // output headers
+    for (size_t q = 0; q < outs.size(); ++q) {
+      const int o = outs[q];
+      put(moff[o]);
+      put(mR[o]);
+      put(mC[o]);
+      put(rl_at[mem[o].second.front()]);
+      put(rr_at[mem[o].second.back()] + mC[o]);
+      put(pbeg[q]);
+      put(pend[q]);
+    }
+    ln.a0 = (int64_t)H.size();  // work items, most work first
+    std::vector<std::pair<int64_t, int>> ord(outs.size());
+    for (size_t q = 0; q < outs.size(); ++q) {
+      int64_t w = 0;
+      for (size_t t = 0; t < pl[q].size(); ++t) w += 1;
+      ord[q] = {-(w * mR[outs[q]] * mC[outs[q]]), (int)q};
+    }
+    std::stable_sort(ord.begin(), ord.end());
+    int64_t items = 0;
+    for (auto& oq : ord) {
+      const int q = oq.second, o = outs[q];
+      const int rpi = std::max(1, 256 / std::max(1, mC[o]));
+      for (int r0 = 0; r0 < mR[o]; r0 += rpi) {
+        put(q);
+        put(r0);
+        put(std::min(rpi, mR[o] - r0));
+        ++items;
+      }
+    }
+    ln.n0 = items;
+    L.push_back(ln);
+  };
+  // dense launch over root outputs: pairs (X offset, Y offset)
+  auto root_launch = [&](int X, int Y, int Z, int D, double alpha, double beta, double gamma,
+                         const std::vector<int>& outs, const std::vector<std::vector<int>>& px,
+                         const std::vector<std::vector<int>>& py) {
+    if (outs.empty()) return;
+    Launch ln{0, X, Y, Z, D, alpha, beta, gamma, 0, 0, 0, 0, 0, (int64_t)outs.size()};
+    ln.a0 = (int64_t)H.size();
+    for (int o : outs) put(moff[o]);
+    ln.a1 = (int64_t)H.size();
+    for (size_t q = 0; q < outs.size(); ++q) put(1);
+    ln.a2 = (int64_t)H.size();
+    int acc = 0;
+    put(0);
+    for (size_t q = 0; q < outs.size(); ++q) put(acc += (int)px[q].size());
+    ln.a3 = (int64_t)H.size();
+    for (auto& v : px)
+      for (int x : v) put(x);
+    ln.a4 = (int64_t)H.size();
+    for (auto& v : py)
+      for (int y : v) put(y);
+    L.push_back(ln);
+  };
+  // product over members of [g0, g1) (or `only`): Z = alpha X Y + beta D + gamma I
   auto product = [&](int g0, int g1, int X, int Y, int Z, int D, double alpha, double beta,
-                     double gamma, const std::vector<int>* only) {
-    Launch ln{0, X, Y, Z, D, alpha, beta, gamma, 0, 0, 0, 0, 0};
+                     double gamma, const std::vector<int>* only, bool skip_first_split) {
     std::vector<int> outs;
     if (only) outs = *only;
     else
       for (int i = g0; i < g1; ++i) outs.push_back(i);
-    // longest pair lists first (load balance)
-    std::vector<std::vector<std::pair<int, int>>> pl(outs.size());
-    for (size_t q = 0; q < outs.size(); ++q)
-      for (auto& pr : splits[outs[q]])
-        if (mlen(mem[pr.first]) <= nz[X] && mlen(mem[pr.second]) <= nz[Y]) pl[q].push_back(pr);
-    std::vector<int> ord(outs.size());
-    for (size_t q = 0; q < ord.size(); ++q) ord[q] = (int)q;
-    std::stable_sort(ord.begin(), ord.end(),
-                     [&](int a, int b) { return pl[a].size() > pl[b].size(); });
-    ln.nout = (int64_t)outs.size();
-    ln.out_at = (int64_t)H.size();
-    for (int q : ord) put(outs[q] | (mlen(mem[outs[q]]) == 1 ? IDENT : 0));
-    ln.pofs_at = (int64_t)H.size();
-    int acc = 0;
-    put(0);
-    for (int q : ord) put(acc += (int)pl[q].size());
-    ln.px_at = (int64_t)H.size();
-    for (int q : ord)
-      for (auto& pr : pl[q]) put(pr.first);
-    ln.py_at = (int64_t)H.size();
-    for (int q : ord)
-      for (auto& pr : pl[q]) put(pr.second);
-    L.push_back(ln);
+    std::vector<int> routs, couts;
+    std::vector<std::vector<int>> rpx, rpy, cls;
+    std::vector<std::vector<std::pair<int, int>>> cpl;
+    for (int o : outs) {
+      std::vector<std::pair<int, int>> pl;
+      std::vector<int> ls;
+      const auto& sp = splits[o];
+      for (size_t l = skip_first_split ? 1 : 0; l < sp.size(); ++l)
+        if (mlen(mem[sp[l].first]) <= nz[X] && mlen(mem[sp[l].second]) <= nz[Y]) {
+          pl.push_back(sp[l]);
+          ls.push_back((int)l);
+        }
+      if (mlen(mem[o]) == 1) {
+        routs.push_back(o);
+        rpx.emplace_back();
+        rpy.emplace_back();
+        for (auto& pr : pl) {
+          rpx.back().push_back(moff[pr.first]);
+          rpy.back().push_back(moff[pr.second]);
+        }
+      } else {
+        couts.push_back(o);
+        cpl.push_back(pl);
+        cls.push_back(ls);
+      }
+    }
+    root_launch(X, Y, Z, D, alpha, beta, gamma, routs, rpx, rpy);
+    compact_launch(X, Y, Z, D, alpha, beta, couts, cpl, cls, -1);
     int zz = std::min(maxlen, nz[X] + nz[Y] - 1);
     if (D >= 0) zz = std::max(zz, nz[D]);
     if (gamma != 0.0) zz = std::max(zz, 1);
@@ -499,12 +759,11 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
   };
   auto lincomb = [&](int g0, int g1, int Z, std::vector<int> in, std::vector<double> c,
                      double cI) {
-    Launch ln{1, -1, -1, Z, -1, cI, 0.0, 0.0, 0, 0, 0, 0, 0};
-    ln.out_at = (int64_t)H.size();
+    Launch ln{1, -1, -1, Z, -1, cI, 0.0, 0.0, 0, 0, 0, 0, 0, 0};
+    ln.a0 = (int64_t)H.size();
     put(g0);
     put(g1);
     for (int t = 0; t < 4; ++t) put(t < (int)in.size() ? in[t] : -1);
-    ln.pofs_at = (int64_t)H.size();  // coefficients follow in the double table
     L.push_back(ln);
     int zz = cI != 0.0 ? 1 : 0;
     for (int b : in) zz = std::max(zz, nz[b]);
@@ -520,22 +779,23 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
     while (g0 + nroots < g1 && mlen(mem[g0 + nroots]) == 1) ++nroots;
     nz[0] = std::min(2, maxlen);
     // A2
-    product(g0, g1, 0, 0, 1, -1, 1.0, 0.0, 0.0, nullptr);
+    product(g0, g1, 0, 0, 1, -1, 1.0, 0.0, 0.0, nullptr, false);
     if (m == 13) {
       const double* b = kB13;
-      product(g0, g1, 1, 1, 2, -1, 1.0, 0.0, 0.0, nullptr);  // A4
-      product(g0, g1, 1, 2, 3, -1, 1.0, 0.0, 0.0, nullptr);  // A6 = A2 A4
+      product(g0, g1, 1, 1, 2, -1, 1.0, 0.0, 0.0, nullptr, false);  // A4
+      product(g0, g1, 1, 2, 3, -1, 1.0, 0.0, 0.0, nullptr, false);  // A6 = A2 A4
       coefs.push_back(lincomb(g0, g1, 4, {3, 2, 1}, {b[13], b[11], b[9]}, 0.0));
       coefs.push_back(lincomb(g0, g1, 5, {3, 2, 1}, {b[7], b[5], b[3]}, b[1]));
-      product(g0, g1, 3, 4, 6, 5, 1.0, 1.0, 0.0, nullptr);
-      product(g0, g1, 0, 6, 7, -1, 1.0, 0.0, 0.0, nullptr);  // U
+      product(g0, g1, 3, 4, 6, 5, 1.0, 1.0, 0.0, nullptr, false);
+      product(g0, g1, 0, 6, 7, -1, 1.0, 0.0, 0.0, nullptr, false);  // U
       coefs.push_back(lincomb(g0, g1, 4, {3, 2, 1}, {b[12], b[10], b[8]}, 0.0));
       coefs.push_back(lincomb(g0, g1, 5, {3, 2, 1}, {b[6], b[4], b[2]}, b[0]));
-      product(g0, g1, 3, 4, 6, 5, 1.0, 1.0, 0.0, nullptr);  // V
+      product(g0, g1, 3, 4, 6, 5, 1.0, 1.0, 0.0, nullptr, false);  // V
     } else {
       const double* b = m == 3 ? kB3 : m == 5 ? kB5 : m == 7 ? kB7 : kB9;
       const int np = m / 2;
-      for (int p = 2; p <= np; ++p) product(g0, g1, p - 1, 1, p, -1, 1.0, 0.0, 0.0, nullptr);
+      for (int p = 2; p <= np; ++p)
+        product(g0, g1, p - 1, 1, p, -1, 1.0, 0.0, 0.0, nullptr, false);
       std::vector<int> P{1};
       std::vector<double> cu{b[3]}, cv{b[2]};
       for (int p = 2; p <= np; ++p) {
@@ -544,16 +804,16 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
         cv.push_back(b[2 * p]);
       }
       coefs.push_back(lincomb(g0, g1, 5, P, cu, b[1]));
-      product(g0, g1, 0, 5, 7, -1, 1.0, 0.0, 0.0, nullptr);  // U
-      coefs.push_back(lincomb(g0, g1, 6, P, cv, b[0]));      // V
+      product(g0, g1, 0, 5, 7, -1, 1.0, 0.0, 0.0, nullptr, false);  // U
+      coefs.push_back(lincomb(g0, g1, 6, P, cv, b[0]));              // V
     }
     // M = V - U (W1), N = V + U (W2)
     coefs.push_back(lincomb(g0, g1, 1, {6, 7}, {1.0, -1.0}, 0.0));
     coefs.push_back(lincomb(g0, g1, 2, {6, 7}, {1.0, 1.0}, 0.0));
     // inverse of each interval's diagonal block (the roots, members g0 .. g0+nroots)
     {
-      Launch ln{2, 1, -1, NINV, -1, 0.0, 0.0, 0.0, 0, 0, 0, 0, 0};
-      ln.out_at = (int64_t)H.size();
+      Launch ln{2, 1, -1, NINV, -1, 0.0, 0.0, 0.0, 0, 0, 0, 0, 0, 0};
+      ln.a0 = (int64_t)H.size();
       put(g0);
       put(nroots);
       L.push_back(ln);
@@ -566,29 +826,27 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
         if (mlen(mem[i]) == len) outs.push_back(i);
       if (outs.empty()) continue;
       if (len > 1) {
-        // pairs l >= 1 only: X member length >= 2
-        std::vector<std::vector<std::pair<int, int>>> save(outs.size());
-        for (size_t q = 0; q < outs.size(); ++q) {
-          save[q] = splits[outs[q]];
-          splits[outs[q]].erase(splits[outs[q]].begin());
-        }
-        nz[1] = maxlen;
+        nz[1] = maxlen;  // pairs l >= 1 only: X member length >= 2
         nz[3] = len - 1;
-        product(g0, g1, 1, 3, 2, 2, -1.0, 1.0, 0.0, &outs);
-        for (size_t q = 0; q < outs.size(); ++q) splits[outs[q]] = save[q];
+        product(g0, g1, 1, 3, 2, 2, -1.0, 1.0, 0.0, &outs, true);
       }
       // R[s] = inv[interval of s] N[s]: one pair per member
-      Launch ln{0, NINV, 2, 3, -1, 1.0, 0.0, 0.0, 0, 0, 0, 0, 0};
-      ln.nout = (int64_t)outs.size();
-      ln.out_at = (int64_t)H.size();
-      for (int o : outs) put(o);
-      ln.pofs_at = (int64_t)H.size();
-      for (size_t q = 0; q <= outs.size(); ++q) put((int)q);
-      ln.px_at = (int64_t)H.size();
-      for (int o : outs) put(root_of(mem[o].first) - g0);  // inverse slot
-      ln.py_at = (int64_t)H.size();
-      for (int o : outs) put(o);
-      L.push_back(ln);
+      if (len == 1) {
+        std::vector<std::vector<int>> px(outs.size()), py(outs.size());
+        for (size_t q = 0; q < outs.size(); ++q) {
+          px[q].push_back((int)((root_of(mem[outs[q]].first) - g0) * nn));
+          py[q].push_back(moff[outs[q]]);
+        }
+        root_launch(NINV, 2, 3, -1, 1.0, 0.0, 0.0, outs, px, py);
+      } else {
+        std::vector<std::vector<std::pair<int, int>>> pl(outs.size());
+        std::vector<std::vector<int>> ls(outs.size());
+        for (size_t q = 0; q < outs.size(); ++q) {
+          pl[q].push_back({-1, outs[q]});
+          ls[q].push_back(0);
+        }
+        compact_launch(NINV, 2, 3, -1, 1.0, 0.0, outs, pl, ls, g0);
+      }
     }
     nz[3] = maxlen;
     // squarings, in lock-step over the intervals still squaring (W3 <-> W2)
@@ -600,26 +858,38 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
         if (js[mem[i].first] >= lev) outs.push_back(i);
       const int X = (lev & 1) ? 3 : 2, Z = (lev & 1) ? 2 : 3;
       nz[X] = maxlen;
-      product(g0, g1, X, X, Z, -1, 1.0, 0.0, 0.0, &outs);
+      product(g0, g1, X, X, Z, -1, 1.0, 0.0, 0.0, &outs, false);
     }
     for (int i = g0; i < g0 + nroots; ++i) final_sel[mem[i].first] = js[mem[i].first] & 1;
   }
-  // output: path p = member (interval, whole path); W3 or W2 by its squaring parity
-  const int64_t out_idx_at = (int64_t)H.size();
+  // output: path p = member (interval, whole path), W3 or W2 by its squaring parity
+  const int64_t pdesc_at = (int64_t)H.size();
   for (int64_t p = 0; p < npaths; ++p) {
     const int L0 = (int)(h_off[p + 1] - h_off[p]);
-    put(id.at(Key{h_job[p], L0 == 1 ? std::vector<int>()
-                                    : std::vector<int>(h_mask + h_off[p], h_mask + h_off[p + 1])}));
+    const int o = id.at(Key{h_job[p], L0 == 1 ? std::vector<int>()
+                                              : std::vector<int>(h_mask + h_off[p],
+                                                                 h_mask + h_off[p + 1])});
+    put(moff[o]);
+    put(mC[o]);
+    put(L0 == 1 ? 1 : 0);
+    put(L0 == 1 ? 0 : rp_at[h_mask[h_off[p]]]);
+    put(L0 == 1 ? 0 : cp_at[h_mask[h_off[p + 1] - 1]]);
+    put(final_sel[h_job[p]]);
   }
-  const int64_t out_sel_at = (int64_t)H.size();
-  for (int64_t p = 0; p < npaths; ++p) put(final_sel[h_job[p]]);
   // member descriptors for the A build
   const int64_t desc_at = (int64_t)H.size();
+  int64_t maxsize = nn;
   for (int i = 0; i < NM; ++i) {
     const int len = mlen(mem[i]);
     put(len == 1 ? 0 : len == 2 ? 1 : 2);
     put(len == 2 ? mem[i].second[0] : 0);
     put(len == 2 ? mem[i].second[1] : 0);
+    put(moff[i]);
+    put(mR[i]);
+    put(mC[i]);
+    put(len == 1 ? iota_at : rl_at[mem[i].second.front()]);
+    put(len == 1 ? iota_at : rr_at[mem[i].second.back()] + mC[i]);
+    maxsize = std::max(maxsize, (int64_t)mR[i] * mC[i]);
   }
   while (H.size() & 1) put(0);
   // doubles: tau per member, Q, masks
@@ -632,6 +902,7 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
     while (gbeg[gi] + r < gend[gi] && mlen(mem[gbeg[gi] + r]) == 1) ++r;
     maxroots = std::max(maxroots, r);
   }
+  const int64_t W = tot;
   const size_t dbytes = (size_t)(8 * W + (int64_t)maxroots * nn) * sizeof(double) +
                         (size_t)maxroots * nb * sizeof(int) + hbytes + 256;
   Ws* ws = nullptr;
@@ -659,14 +930,13 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
   const double* dd = reinterpret_cast<const double*>(ds + ints);
   if ((e = hipMemcpyAsync(dstage, hs, hbytes, hipMemcpyHostToDevice, st))) return e;
 
-  const int bx = (int)std::min<int64_t>((nn + 255) / 256, 64);
   {
-    BuildArgs a{nb, NM, dd + nd_tau, dd + nd_tau + nd_q, ds + desc_at, dd, Wb[0]};
+    const int bx = (int)std::min<int64_t>((maxsize + 255) / 256, 64);
+    BuildArgs a{nb, dd + nd_tau, dd + nd_tau + nd_q, ds + desc_at, ds, dd, Wb[0]};
     for (int64_t m0 = 0; m0 < NM; m0 += 65535) {
       BuildArgs h = a;
-      h.desc += 3 * m0;
+      h.desc += kMD * m0;
       h.tau += 2 * m0;
-      h.A += m0 * nn;
       hipLaunchKernelGGL(build_members_kernel,
                          dim3(bx, (unsigned)std::min<int64_t>(65535, NM - m0)), dim3(256), 0, st,
                          h);
@@ -677,7 +947,7 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
   size_t ci = 0;
   for (const Launch& ln : L) {
     if (ln.kind == 0) {
-      if (ln.nout == 0) continue;
+      if (ln.n0 == 0) continue;
       PairGemmArgs g{};
       g.nb = nb;
       g.tn = tn;
@@ -688,59 +958,76 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
       g.alpha = ln.alpha;
       g.beta = ln.beta;
       g.gamma = ln.gamma;
-      const int64_t chunk = ((int64_t)1 << 30) / (tn * tn);  // grid.x limit
-      for (int64_t o0 = 0; o0 < ln.nout; o0 += chunk) {
-        PairGemmArgs h = g;
-        h.nout = std::min<int64_t>(chunk, ln.nout - o0);
-        h.out = ds + ln.out_at + o0;
-        h.pofs = ds + ln.pofs_at + o0;
-        h.px = ds + ln.px_at;
-        h.py = ds + ln.py_at;
-        const int64_t total = h.nout * tn * tn;
-        const unsigned grid = (unsigned)((total + 7) / 8 * 8);
-        hipLaunchKernelGGL(pair_gemm_kernel, dim3(grid), dim3(256), 0, st, h);
+      g.nout = ln.n0;
+      g.zoff = ds + ln.a0;
+      g.zid = ds + ln.a1;
+      g.pofs = ds + ln.a2;
+      g.px = ds + ln.a3;
+      g.py = ds + ln.a4;
+      const int64_t total = g.nout * tn * tn;
+      const unsigned grid = (unsigned)((total + 7) / 8 * 8);
+      hipLaunchKernelGGL(pair_gemm_kernel, dim3(grid), dim3(256), 0, st, g);
+    } else if (ln.kind == 4) {
+      if (ln.n0 == 0) continue;
+      CompactArgs a{};
+      a.nb = nb;
+      a.items = ds + ln.a0;
+      a.ohdr = ds + ln.a1;
+      a.phdr = ds + ln.a2;
+      a.tab = ds;
+      a.X = Wb[ln.x];
+      a.Y = Wb[ln.y];
+      a.Z = Wb[ln.z];
+      a.D = ln.d >= 0 ? Wb[ln.d] : nullptr;
+      a.alpha = ln.alpha;
+      a.beta = ln.beta;
+      for (int64_t i0 = 0; i0 < ln.n0; i0 += ((int64_t)1 << 30)) {
+        CompactArgs h = a;
+        h.nitems = (int)std::min<int64_t>((int64_t)1 << 30, ln.n0 - i0);
+        h.items += 3 * i0;
+        hipLaunchKernelGGL(compact_gemm_kernel, dim3(h.nitems), dim3(256), 0, st, h);
       }
     } else if (ln.kind == 1) {
-      const int g0 = H[ln.out_at], g1 = H[ln.out_at + 1];
+      const int g0 = H[ln.a0], g1 = H[ln.a0 + 1];
       const std::vector<double>& c = coefs[ci++];
       LinArgs a{};
       a.nb = nb;
-      a.count = g1 - g0;
-      a.out = Wb[ln.z] + (int64_t)g0 * nn;
+      a.count = (int64_t)moff[g1] - moff[g0];
+      a.out = Wb[ln.z] + moff[g0];
       int nr = 0;
       while (g0 + nr < g1 && mlen(mem[g0 + nr]) == 1) ++nr;
-      a.nident = nr;
+      a.nident = nr * nn;
       for (int t = 0; t < 4; ++t) {
-        const int b = H[ln.out_at + 2 + t];
-        a.in[t] = b >= 0 ? Wb[b] + (int64_t)g0 * nn : nullptr;
+        const int b = H[ln.a0 + 2 + t];
+        a.in[t] = b >= 0 ? Wb[b] + moff[g0] : nullptr;
         a.c[t] = t < (int)c.size() ? c[t] : 0.0;
       }
       a.cI = ln.alpha;
-      const int64_t total = a.count * nn;
-      const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 64);
+      const unsigned grid = (unsigned)std::min<int64_t>((a.count + 255) / 256, 256 * 64);
       hipLaunchKernelGGL(member_lincomb_kernel, dim3(grid), dim3(256), 0, st, a);
     } else if (ln.kind == 2) {
-      const int g0 = H[ln.out_at], nr = H[ln.out_at + 1];
+      const int g0 = H[ln.a0], nr = H[ln.a0 + 1];
       LinArgs a{};
       a.nb = nb;
-      a.count = nr;
-      a.nident = nr;
+      a.count = nr * nn;
+      a.nident = nr * nn;
       a.out = Wb[NINV];
       a.cI = 1.0;
       hipLaunchKernelGGL(member_lincomb_kernel,
                          dim3((unsigned)std::min<int64_t>((nr * nn + 255) / 256, 4096)),
                          dim3(256), 0, st, a);
-      if ((e = solve_batched(nb, nb, nr, Wb[1] + (int64_t)g0 * nn, Wb[NINV], piv, st)))
-        return e;
+      if ((e = solve_batched(nb, nb, nr, Wb[1] + moff[g0], Wb[NINV], piv, st))) return e;
     }
     if ((e = hipGetLastError())) return e;
   }
-  for (int64_t p0 = 0; p0 < npaths; p0 += 65535)
-    hipLaunchKernelGGL(gather_members_kernel,
-                       dim3(bx, (unsigned)std::min<int64_t>(65535, npaths - p0)), dim3(256), 0,
-                       st, nb, Wb[3], Wb[2], ds + out_idx_at + p0, ds + out_sel_at + p0,
-                       d_out + p0 * nn);
-  if ((e = hipGetLastError())) return e;
+  {
+    const int bx = (int)std::min<int64_t>((nn + 255) / 256, 64);
+    for (int64_t p0 = 0; p0 < npaths; p0 += 65535)
+      hipLaunchKernelGGL(scatter_paths_kernel,
+                         dim3(bx, (unsigned)std::min<int64_t>(65535, npaths - p0)), dim3(256), 0,
+                         st, nb, Wb[3], Wb[2], ds + pdesc_at + kPD * p0, ds, d_out + p0 * nn);
+    if ((e = hipGetLastError())) return e;
+  }
   // the workspace and the staging buffer are free again once everything above has run: the
   // next call (ws_get) waits for this, whichever stream it is issued on (the model build
   // prefetches one evaluation on a side stream while others run on the main stream)

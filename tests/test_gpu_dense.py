@@ -146,3 +146,55 @@ def test_vanloan_paths_shared_matches_per_path(gpu, n, nmask):
         ref = sl.expm(C * t[j])[:n, -n:]
         scale = max(np.abs(ref).max(), 1e-300)
         assert np.abs(got[k] - ref).max() <= 1e-11 * max(scale, 1.0), (k, j, L)
+
+
+@pytest.mark.parametrize("n,ncls", [(40, 5), (203, 16)])
+def test_vanloan_paths_compact_supports(gpu, n, ncls):
+    """The support-compressed evaluation on a nearly acyclic CTMC like the coalescent ones:
+    states in ordered classes, transitions only within a class or to later classes, masks
+    = classes.  Non-root members then live on small rectangles (rows reaching the first
+    class, columns reached from the last); the result matches scipy's expm of every path's
+    block matrix, including the exact zeros outside the rectangle.  A subset of the paths
+    evaluated with the norms of the whole set (the rank-split build) gives the same matrices
+    bit for bit."""
+    import scipy.linalg as sl
+    from itrails_amd.dense import vanloan_job_norms, vanloan_paths
+    rng = np.random.default_rng(7 * n + ncls)
+    cls = np.sort(rng.integers(0, ncls, n))
+    Q = rng.random((n, n)) * (rng.random((n, n)) < 0.25)
+    Q *= cls[None, :] >= cls[:, None]  # no transition back to an earlier class
+    np.fill_diagonal(Q, 0.0)
+    np.fill_diagonal(Q, -Q.sum(axis=1))
+    Q /= max(1.0, np.abs(Q).sum(axis=0).max())
+    masks = np.stack([(cls == c).astype(np.uint8) for c in range(ncls)])
+    t = np.array([0.3, 2.5, 40.0])
+    paths = []
+    for _ in range(60):
+        L = int(rng.integers(1, 6))
+        seq = np.sort(rng.choice(ncls, L, replace=L > ncls))
+        paths.append((int(rng.integers(0, 3)), [int(x) for x in seq]))
+    job = np.array([j for j, _ in paths], dtype=np.int32)
+    off = np.zeros(len(paths) + 1, dtype=np.int64)
+    np.cumsum([len(p) for _, p in paths], out=off[1:])
+    pm = np.array([w for _, p in paths for w in p], dtype=np.int32)
+    got = vanloan_paths(Q, t, masks, job, off, pm).cpu().numpy()
+    for k, (j, p) in enumerate(paths):
+        L = len(p)
+        C = np.zeros((n * L, n * L))
+        for b in range(L):
+            C[b * n:(b + 1) * n, b * n:(b + 1) * n] = Q
+        for b in range(1, L):
+            C[(b - 1) * n:b * n, b * n:(b + 1) * n] = masks[p[b - 1]][:, None] * Q * \
+                masks[p[b]][None, :]
+        ref = sl.expm(C * t[j])[:n, -n:]
+        scale = max(np.abs(ref).max(), 1e-300)
+        assert np.abs(got[k] - ref).max() <= 1e-11 * max(scale, 1.0), (k, j, L)
+        assert not got[k][ref == 0.0].any(), (k, "non-zero outside the support")
+    # a subset with the whole set's norms: same branch, bit-identical matrices
+    norms = vanloan_job_norms(Q, t, masks, job, off, pm)
+    sel = np.arange(0, len(paths), 3)
+    soff = np.zeros(len(sel) + 1, dtype=np.int64)
+    np.cumsum([len(paths[i][1]) for i in sel], out=soff[1:])
+    spm = np.array([w for i in sel for w in paths[i][1]], dtype=np.int32)
+    sub = vanloan_paths(Q, t, masks, job[sel], soff, spm, job_norm=norms).cpu().numpy()
+    assert np.array_equal(sub, got[sel])
