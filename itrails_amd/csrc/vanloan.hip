@@ -45,6 +45,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <deque>
 #include <map>
 #include <vector>
 
@@ -354,6 +355,31 @@ void branch_of(double norm, int* m, int* s) {  // expm.py:26-143
   }
 }
 
+struct Launch {
+  int kind;  // 0 dense root product, 1 lincomb, 2 invert roots, 4 compact product
+  int x, y, z, d;  // buffer ids (-1 none); NINV = the root inverses
+  double alpha, beta, gamma;
+  int64_t a0, a1, a2, a3, a4;  // descriptor offsets in H
+  int64_t n0;                  // outputs / work items
+};
+
+struct VlPlan {
+  // key: the request's structure
+  int nb = 0, njobs = 0, nmasks = 0;
+  std::vector<int32_t> job, mask;
+  std::vector<int64_t> off;
+  std::vector<uint8_t> masks;
+  std::vector<uint64_t> qpat;  // Q != 0, bit rows
+  std::vector<int> jm, js;
+  // plan
+  std::vector<int> H;  // device descriptor ints (support table first)
+  std::vector<Launch> L;
+  std::vector<std::vector<double>> coefs;  // per lincomb launch
+  std::vector<int> mjob, moff;
+  int NM = 0, maxroots = 0;
+  int64_t tot = 0, maxsize = 0, pdesc_at = 0, desc_at = 0;
+};
+
 // grow-only device workspace and pinned staging, per device and calling thread (two threads
 // evaluating on one device must not share the staging buffer or the workspace); a call
 // waits for the previous call of its thread on that device (`done`) before reusing them
@@ -379,6 +405,7 @@ struct WsSet {
   ~WsSet() { release(); }
 };
 thread_local WsSet g_ws;
+thread_local std::deque<VlPlan> g_plans;  // recent launch plans of this thread
 
 hipError_t ws_get(size_t dbytes, size_t hbytes, Ws** out) {
   int dev = 0;
@@ -412,7 +439,10 @@ hipError_t ws_get(size_t dbytes, size_t hbytes, Ws** out) {
 
 }  // namespace
 
-void release_vanloan_workspace() { g_ws.release(); }
+void release_vanloan_workspace() {
+  g_ws.release();
+  g_plans.clear();
+}
 
 void vanloan_job_norms(int nb, const double* h_Q, int njobs, const double* h_t, int nmasks,
                        const uint8_t* h_masks, int64_t npaths, const int32_t* h_job,
@@ -422,7 +452,10 @@ void vanloan_job_norms(int nb, const double* h_Q, int njobs, const double* h_t, 
     for (int c = 0; c < nb; ++c) cs[c] += fabs(h_Q[(int64_t)r * nb + c]);
   // per mask a: (m_a^T |Q|)[c]; a pair's column sums are cs[c] + m_b[c] (m_a^T |Q|)[c]
   std::vector<std::vector<double>> mq(nmasks);
+  std::vector<double> memo((size_t)nmasks * nmasks, -1.0);  // pair norms, computed once
   auto pnorm = [&](int a, int b) -> double {
+    double& slot = memo[(size_t)a * nmasks + b];
+    if (slot >= 0.0) return slot;
     if (mq[a].empty()) {
       mq[a].assign(nb, 0.0);
       const uint8_t* ma = h_masks + (int64_t)a * nb;
@@ -433,7 +466,7 @@ void vanloan_job_norms(int nb, const double* h_Q, int njobs, const double* h_t, 
     const uint8_t* mb = h_masks + (int64_t)b * nb;
     double best = 0.0;
     for (int c = 0; c < nb; ++c) best = std::max(best, cs[c] + (mb[c] ? mq[a][c] : 0.0));
-    return best;
+    return slot = best;
   };
   const double cmax = *std::max_element(cs.begin(), cs.end());
   for (int j = 0; j < njobs; ++j) jnorm[j] = 0.0;
@@ -447,26 +480,14 @@ void vanloan_job_norms(int nb, const double* h_Q, int njobs, const double* h_t, 
   }
 }
 
-hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t, int nmasks,
-                         const uint8_t* h_masks, int64_t npaths, const int32_t* h_job,
-                         const int64_t* h_off, const int32_t* h_mask, const double* h_jnorm,
-                         double* d_out, hipStream_t st) {
-  if (npaths <= 0) return hipSuccess;
+// The launch plan of one request: depends only on the path structure, the masks, Q's zero
+// pattern and each interval's Pade branch and squaring count — not on Q's values or the
+// interval lengths — so the optimizer's repeated rebuilds reuse it (plan cache below).
+static hipError_t build_plan(VlPlan& P, int nb, const double* h_Q, int njobs, int nmasks,
+                             const uint8_t* h_masks, int64_t npaths, const int32_t* h_job,
+                             const int64_t* h_off, const int32_t* h_mask,
+                             const std::vector<int>& jm, const std::vector<int>& js, int maxlen) {
   const int64_t nn = (int64_t)nb * nb;
-
-  // ---- norms -> Pade branch and scaling per interval (expm.py:16-143); a caller that
-  // evaluates a subset of an interval's paths (the rank-split build) passes the norms of the
-  // whole set so that every subset takes the same branch and scaling ----------------------
-  std::vector<double> jnorm(njobs, 0.0);
-  vanloan_job_norms(nb, h_Q, njobs, h_t, nmasks, h_masks, npaths, h_job, h_off, h_mask,
-                    jnorm.data());
-  if (h_jnorm)
-    for (int j = 0; j < njobs; ++j) jnorm[j] = std::max(jnorm[j], h_jnorm[j]);
-  int maxlen = 1;
-  for (int64_t p = 0; p < npaths; ++p) maxlen = std::max(maxlen, (int)(h_off[p + 1] - h_off[p]));
-  std::vector<int> jm(njobs, 13), js(njobs, 0);
-  for (int j = 0; j < njobs; ++j) branch_of(jnorm[j], &jm[j], &js[j]);
-
   // ---- supports: transitive closure of Q's transition graph (bit rows, Warshall) ---------
   const int NW = (nb + 63) / 64;
   std::vector<uint64_t> reach((size_t)nb * NW, 0);
@@ -608,13 +629,6 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
   auto put = [&](int v) {
     H.push_back(v);
     return (int64_t)H.size() - 1;
-  };
-  struct Launch {
-    int kind;  // 0 dense root product, 1 lincomb, 2 invert roots, 4 compact product
-    int x, y, z, d;  // buffer ids (-1 none); NINV = the root inverses
-    double alpha, beta, gamma;
-    int64_t a0, a1, a2, a3, a4;  // descriptor offsets in H
-    int64_t n0;                  // outputs / work items
   };
   std::vector<Launch> L;
   int nz[9];
@@ -760,6 +774,7 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
   auto lincomb = [&](int g0, int g1, int Z, std::vector<int> in, std::vector<double> c,
                      double cI) {
     Launch ln{1, -1, -1, Z, -1, cI, 0.0, 0.0, 0, 0, 0, 0, 0, 0};
+    while (g0 + ln.n0 < g1 && mlen(mem[g0 + ln.n0]) == 1) ++ln.n0;  // leading roots
     ln.a0 = (int64_t)H.size();
     put(g0);
     put(g1);
@@ -892,27 +907,106 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
     maxsize = std::max(maxsize, (int64_t)mR[i] * mC[i]);
   }
   while (H.size() & 1) put(0);
-  // doubles: tau per member, Q, masks
-  const int64_t nd_tau = 2 * (int64_t)NM, nd_q = nn, nd_m = (int64_t)nmasks * nb;
-  const int64_t ints = (int64_t)H.size();
-  const size_t hbytes = ints * sizeof(int) + (nd_tau + nd_q + nd_m) * sizeof(double);
-  int maxroots = 0;
+  P.maxroots = 0;
   for (size_t gi = 0; gi < groups_m.size(); ++gi) {
     int r = 0;
     while (gbeg[gi] + r < gend[gi] && mlen(mem[gbeg[gi] + r]) == 1) ++r;
-    maxroots = std::max(maxroots, r);
+    P.maxroots = std::max(P.maxroots, r);
   }
-  const int64_t W = tot;
+  P.NM = NM;
+  P.tot = tot;
+  P.maxsize = maxsize;
+  P.pdesc_at = pdesc_at;
+  P.desc_at = desc_at;
+  P.mjob.resize(NM);
+  for (int i = 0; i < NM; ++i) P.mjob[i] = mem[i].first;
+  P.moff = std::move(moff);
+  P.H = std::move(H);
+  P.L = std::move(L);
+  P.coefs = std::move(coefs);
+  return hipSuccess;
+}
+
+hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t, int nmasks,
+                         const uint8_t* h_masks, int64_t npaths, const int32_t* h_job,
+                         const int64_t* h_off, const int32_t* h_mask, const double* h_jnorm,
+                         double* d_out, hipStream_t st) {
+  if (npaths <= 0) return hipSuccess;
+  const int64_t nn = (int64_t)nb * nb;
+
+  // ---- norms -> Pade branch and scaling per interval (expm.py:16-143); a caller that
+  // evaluates a subset of an interval's paths (the rank-split build) passes the norms of the
+  // whole set so that every subset takes the same branch and scaling ----------------------
+  std::vector<double> jnorm(njobs, 0.0);
+  vanloan_job_norms(nb, h_Q, njobs, h_t, nmasks, h_masks, npaths, h_job, h_off, h_mask,
+                    jnorm.data());
+  if (h_jnorm)
+    for (int j = 0; j < njobs; ++j) jnorm[j] = std::max(jnorm[j], h_jnorm[j]);
+  int maxlen = 1;
+  for (int64_t p = 0; p < npaths; ++p) maxlen = std::max(maxlen, (int)(h_off[p + 1] - h_off[p]));
+  std::vector<int> jm(njobs, 13), js(njobs, 0);
+  for (int j = 0; j < njobs; ++j) branch_of(jnorm[j], &jm[j], &js[j]);
+
+  // ---- the plan: cached per thread by the request's structure ---------------------------
+  const int NW = (nb + 63) / 64;
+  std::vector<uint64_t> qpat((size_t)nb * NW, 0);
+  for (int r = 0; r < nb; ++r)
+    for (int c = 0; c < nb; ++c)
+      if (h_Q[(int64_t)r * nb + c] != 0.0) qpat[(size_t)r * NW + (c >> 6)] |= 1ull << (c & 63);
+  const int64_t nmask_ids = h_off[npaths];
+  VlPlan* hit = nullptr;
+  for (VlPlan& c : g_plans) {
+    if (c.nb == nb && c.njobs == njobs && c.nmasks == nmasks &&
+        (int64_t)c.job.size() == npaths && (int64_t)c.mask.size() == nmask_ids &&
+        std::equal(c.job.begin(), c.job.end(), h_job) &&
+        std::equal(c.off.begin(), c.off.end(), h_off) &&
+        std::equal(c.mask.begin(), c.mask.end(), h_mask) &&
+        std::equal(c.masks.begin(), c.masks.end(), h_masks) && c.qpat == qpat && c.jm == jm &&
+        c.js == js) {
+      hit = &c;
+      break;
+    }
+  }
+  if (!hit) {
+    if (g_plans.size() >= 4) g_plans.pop_front();
+    g_plans.emplace_back();
+    VlPlan& c = g_plans.back();
+    c.nb = nb;
+    c.njobs = njobs;
+    c.nmasks = nmasks;
+    c.job.assign(h_job, h_job + npaths);
+    c.off.assign(h_off, h_off + npaths + 1);
+    c.mask.assign(h_mask, h_mask + nmask_ids);
+    c.masks.assign(h_masks, h_masks + (int64_t)nmasks * nb);
+    c.qpat = qpat;
+    c.jm = jm;
+    c.js = js;
+    if (hipError_t e = build_plan(c, nb, h_Q, njobs, nmasks, h_masks, npaths, h_job, h_off,
+                                  h_mask, jm, js, maxlen)) {
+      g_plans.pop_back();
+      return e;
+    }
+    hit = &c;
+  }
+  const VlPlan& P = *hit;
+
+  // doubles: tau per member, Q, masks
+  const int64_t nd_tau = 2 * (int64_t)P.NM, nd_q = nn, nd_m = (int64_t)nmasks * nb;
+  const int64_t ints = (int64_t)P.H.size();
+  const size_t hbytes = ints * sizeof(int) + (nd_tau + nd_q + nd_m) * sizeof(double);
+  const int maxroots = P.maxroots;
+  const int NINV = 8;
+  const int64_t W = P.tot;
   const size_t dbytes = (size_t)(8 * W + (int64_t)maxroots * nn) * sizeof(double) +
                         (size_t)maxroots * nb * sizeof(int) + hbytes + 256;
   Ws* ws = nullptr;
   hipError_t e = ws_get(dbytes, hbytes, &ws);
   if (e) return e;
   int* hs = ws->h;
-  std::copy(H.begin(), H.end(), hs);
+  std::copy(P.H.begin(), P.H.end(), hs);
   double* hd = reinterpret_cast<double*>(hs + ints);
-  for (int i = 0; i < NM; ++i) {
-    const int j = mem[i].first;
+  for (int i = 0; i < P.NM; ++i) {
+    const int j = P.mjob[i];
     hd[2 * i] = h_t[j];
     hd[2 * i + 1] = ldexp(1.0, -js[j]);
   }
@@ -931,21 +1025,21 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
   if ((e = hipMemcpyAsync(dstage, hs, hbytes, hipMemcpyHostToDevice, st))) return e;
 
   {
-    const int bx = (int)std::min<int64_t>((maxsize + 255) / 256, 64);
-    BuildArgs a{nb, dd + nd_tau, dd + nd_tau + nd_q, ds + desc_at, ds, dd, Wb[0]};
-    for (int64_t m0 = 0; m0 < NM; m0 += 65535) {
+    const int bx = (int)std::min<int64_t>((P.maxsize + 255) / 256, 64);
+    BuildArgs a{nb, dd + nd_tau, dd + nd_tau + nd_q, ds + P.desc_at, ds, dd, Wb[0]};
+    for (int64_t m0 = 0; m0 < P.NM; m0 += 65535) {
       BuildArgs h = a;
       h.desc += kMD * m0;
       h.tau += 2 * m0;
       hipLaunchKernelGGL(build_members_kernel,
-                         dim3(bx, (unsigned)std::min<int64_t>(65535, NM - m0)), dim3(256), 0, st,
+                         dim3(bx, (unsigned)std::min<int64_t>(65535, P.NM - m0)), dim3(256), 0, st,
                          h);
     }
     if ((e = hipGetLastError())) return e;
   }
   const int tn = (nb + TT - 1) / TT;
   size_t ci = 0;
-  for (const Launch& ln : L) {
+  for (const Launch& ln : P.L) {
     if (ln.kind == 0) {
       if (ln.n0 == 0) continue;
       PairGemmArgs g{};
@@ -988,25 +1082,23 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
         hipLaunchKernelGGL(compact_gemm_kernel, dim3(h.nitems), dim3(256), 0, st, h);
       }
     } else if (ln.kind == 1) {
-      const int g0 = H[ln.a0], g1 = H[ln.a0 + 1];
-      const std::vector<double>& c = coefs[ci++];
+      const int g0 = P.H[ln.a0], g1 = P.H[ln.a0 + 1];
+      const std::vector<double>& c = P.coefs[ci++];
       LinArgs a{};
       a.nb = nb;
-      a.count = (int64_t)moff[g1] - moff[g0];
-      a.out = Wb[ln.z] + moff[g0];
-      int nr = 0;
-      while (g0 + nr < g1 && mlen(mem[g0 + nr]) == 1) ++nr;
-      a.nident = nr * nn;
+      a.count = (int64_t)P.moff[g1] - P.moff[g0];
+      a.out = Wb[ln.z] + P.moff[g0];
+      a.nident = ln.n0 * nn;
       for (int t = 0; t < 4; ++t) {
-        const int b = H[ln.a0 + 2 + t];
-        a.in[t] = b >= 0 ? Wb[b] + moff[g0] : nullptr;
+        const int b = P.H[ln.a0 + 2 + t];
+        a.in[t] = b >= 0 ? Wb[b] + P.moff[g0] : nullptr;
         a.c[t] = t < (int)c.size() ? c[t] : 0.0;
       }
       a.cI = ln.alpha;
       const unsigned grid = (unsigned)std::min<int64_t>((a.count + 255) / 256, 256 * 64);
       hipLaunchKernelGGL(member_lincomb_kernel, dim3(grid), dim3(256), 0, st, a);
     } else if (ln.kind == 2) {
-      const int g0 = H[ln.a0], nr = H[ln.a0 + 1];
+      const int g0 = P.H[ln.a0], nr = P.H[ln.a0 + 1];
       LinArgs a{};
       a.nb = nb;
       a.count = nr * nn;
@@ -1016,7 +1108,7 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
       hipLaunchKernelGGL(member_lincomb_kernel,
                          dim3((unsigned)std::min<int64_t>((nr * nn + 255) / 256, 4096)),
                          dim3(256), 0, st, a);
-      if ((e = solve_batched(nb, nb, nr, Wb[1] + moff[g0], Wb[NINV], piv, st))) return e;
+      if ((e = solve_batched(nb, nb, nr, Wb[1] + P.moff[g0], Wb[NINV], piv, st))) return e;
     }
     if ((e = hipGetLastError())) return e;
   }
@@ -1025,7 +1117,7 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
     for (int64_t p0 = 0; p0 < npaths; p0 += 65535)
       hipLaunchKernelGGL(scatter_paths_kernel,
                          dim3(bx, (unsigned)std::min<int64_t>(65535, npaths - p0)), dim3(256), 0,
-                         st, nb, Wb[3], Wb[2], ds + pdesc_at + kPD * p0, ds, d_out + p0 * nn);
+                         st, nb, Wb[3], Wb[2], ds + P.pdesc_at + kPD * p0, ds, d_out + p0 * nn);
     if ((e = hipGetLastError())) return e;
   }
   // the workspace and the staging buffer are free again once everything above has run: the

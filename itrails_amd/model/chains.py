@@ -39,23 +39,39 @@ def _interval_lengths(cut) -> List[float]:
     return [cut[i + 1] - cut[i] for i in range(len(cut) - 1)]
 
 
+_COMBINE: Dict = {}
+
+
 def combine_states(sd1, sd2, sd_sum, p1: np.ndarray, p2: np.ndarray) -> np.ndarray:
     """Initial vector of the merged chain: product measure of two independent chains, each
-    merged state relabelled by first appearance (combine_states.py:5-90)."""
+    merged state relabelled by first appearance (combine_states.py:5-90).  The relabelling
+    depends only on the three state spaces and is computed once."""
+    key = (id(sd1), id(sd2), id(sd_sum))
+    m = _COMBINE.get(key)
+    if m is None:
+        i1s, i2s, tgt = [], [], []
+        for s1, i1 in sd1.index.items():
+            h1 = len(s1) // 2
+            for s2, i2 in sd2.index.items():
+                h2 = len(s2) // 2
+                seen1, seen2, lab, nxt = {}, {}, [], 1
+                for part, seen in ((s1[:h1], seen1), (s2[:h2], seen2), (s1[h1:], seen1),
+                                   (s2[h2:], seen2)):
+                    for v in part:
+                        if v not in seen:
+                            seen[v] = nxt
+                            nxt += 1
+                        lab.append(seen[v])
+                i1s.append(i1)
+                i2s.append(i2)
+                tgt.append(sd_sum.index[tuple(lab)])
+        m = (np.asarray(i1s), np.asarray(i2s), np.asarray(tgt))
+        if len(set(tgt)) != len(tgt):
+            raise AssertionError("combine_states: relabelling is not one-to-one")
+        _COMBINE[key] = m
+    i1, i2, tgt = m
     out = np.zeros(sd_sum.n, dtype=np.float64)
-    for s1, i1 in sd1.index.items():
-        h1 = len(s1) // 2
-        for s2, i2 in sd2.index.items():
-            h2 = len(s2) // 2
-            seen1, seen2, lab, nxt = {}, {}, [], 1
-            for part, seen in ((s1[:h1], seen1), (s2[:h2], seen2), (s1[h1:], seen1),
-                               (s2[h2:], seen2)):
-                for v in part:
-                    if v not in seen:
-                        seen[v] = nxt
-                        nxt += 1
-                    lab.append(seen[v])
-            out[sd_sum.index[tuple(lab)]] = p1[0, i1] * p2[0, i2]
+    out[tgt] = p1[0, i1] * p2[0, i2]
     return out.reshape(1, -1)
 
 
@@ -79,9 +95,11 @@ def _branch_rows_abc(side, step):
 
 
 def run_chain_ab(Q, times, masks, probs: Dict, n_int, la) -> Dict:
-    """run_markov_chain_AB.py:105-271: two-species chain over the n_int AB intervals."""
+    """run_markov_chain_AB.py:105-271: two-species chain over the n_int AB intervals (every
+    interval's propagator expm(Q dt) requested as one batch up front)."""
+    Es = la.expm([Q * times[step] for step in range(n_int)])
     for step in range(n_int):
-        E = la.expm([Q * times[step]])[0]
+        E = Es[step]
         og = list(probs.keys())
         ogs = set(og)
         updates = []

@@ -148,10 +148,17 @@ def jc69_rate(mu: float) -> np.ndarray:
 
 
 def branch_generator(ts, mus) -> np.ndarray:
-    """sum_k t_k Q_k (p_b_given_a, get_emission_prob_mat.py:22-44), exponentiated later."""
-    mat = np.zeros((4, 4))
+    """sum_k t_k Q_k (p_b_given_a, get_emission_prob_mat.py:22-44), exponentiated later.
+    Every Q_k = jc69_rate(mu_k) has one off-diagonal value mu/4 and one diagonal value
+    mu/4 - mu, so the elementwise sum is two scalar sums in the same order (bit-equal)."""
+    off = 0.0
+    dg = 0.0
     for t, mu in zip(ts, mus):
-        mat = mat + t * jc69_rate(mu)
+        q = mu / 4
+        off = off + t * q
+        dg = dg + t * (q - mu)
+    mat = np.full((4, 4), off)
+    np.fill_diagonal(mat, dg)
     return mat
 
 

@@ -17,6 +17,7 @@ import numpy as np
 Omega = Tuple[int, int]
 
 _SPLIT_GROUP = [None]  # process group of a rank-split model build, see split_build
+_DP_CACHE: Dict = {}  # deepest_t index tensors per (device, paths), see _deepest_plan
 
 
 @contextmanager
@@ -126,31 +127,52 @@ class DeviceLinalg:
         out = torch.empty((len(paths), n, n), dtype=torch.float64, device=self.dev)
         if not len(paths):
             return out
+        plan = self._deepest_plan(masks, paths, n)
         dQ = torch.from_numpy(np.ascontiguousarray(Q)).to(self.dev)
-        eye = torch.eye(n, dtype=torch.float64, device=self.dev)
-        Qinv = solve_batched(dQ[None].clone(), eye[None].clone())[0]
+        Qinv = solve_batched(dQ[None].clone(), plan["eye"][None].clone())[0]
+        A = (plan["ma"][:, :, None] * dQ[None] * plan["mb"][:, None, :]).contiguous()
+        G = gemm_batched(Qinv.expand(A.shape[0], n, n).contiguous(), A)
+        for L, idx, cols in plan["by_len"]:
+            R = G[cols[0]]
+            for k in range(1, L - 1):
+                R = gemm_batched(R.contiguous(), G[cols[k]].contiguous())
+            out[idx] = R if (L - 1) % 2 == 0 else -R
+        self.stats["deepest"] += len(paths)
+        return out
+
+    def _deepest_plan(self, masks, paths, n):
+        """deepest_t's index tensors for one list of paths (the same every rebuild): the
+        distinct omega pairs' mask rows and, per path length, the pair ids of each step."""
+        torch = self.torch
+        key = (str(self.dev), n, tuple(tuple(p) for p in paths), tuple(masks))
+        cache = _DP_CACHE
+        plan = cache.get(key)
+        if plan is not None:
+            return plan
         pair_id: Dict = {}
         for p in paths:
             for i in range(1, len(p)):
                 pair_id.setdefault((p[i - 1], p[i]), len(pair_id))
         pl = list(pair_id)
-        ma = torch.from_numpy(np.stack([masks[a] for a, _ in pl]).astype(np.float64)).to(self.dev)
-        mb = torch.from_numpy(np.stack([masks[b] for _, b in pl]).astype(np.float64)).to(self.dev)
-        A = (ma[:, :, None] * dQ[None] * mb[:, None, :]).contiguous()
-        G = gemm_batched(Qinv.expand(len(pl), n, n).contiguous(), A)
+        dev = self.dev
+        ma = torch.from_numpy(np.stack([masks[a] for a, _ in pl]).astype(np.float64)).to(dev)
+        mb = torch.from_numpy(np.stack([masks[b] for _, b in pl]).astype(np.float64)).to(dev)
         by_len: Dict[int, List[int]] = {}
         for i, p in enumerate(paths):
             by_len.setdefault(len(p), []).append(i)
+        steps = []
         for L, idx in sorted(by_len.items()):
             gi = np.asarray([[pair_id[(paths[i][k - 1], paths[i][k])] for k in range(1, L)]
                              for i in idx], dtype=np.int64)
-            R = G[torch.from_numpy(gi[:, 0]).to(self.dev)]
-            for k in range(1, L - 1):
-                R = gemm_batched(R.contiguous(),
-                                 G[torch.from_numpy(gi[:, k]).to(self.dev)].contiguous())
-            out[torch.as_tensor(idx, device=self.dev)] = R if (L - 1) % 2 == 0 else -R
-        self.stats["deepest"] += len(paths)
-        return out
+            steps.append((L, torch.as_tensor(idx, device=dev),
+                          [torch.from_numpy(np.ascontiguousarray(gi[:, k])).to(dev)
+                           for k in range(L - 1)]))
+        plan = {"ma": ma, "mb": mb, "by_len": steps,
+                "eye": torch.eye(n, dtype=torch.float64, device=dev)}
+        if len(cache) > 8:
+            cache.clear()
+        cache[key] = plan
+        return plan
 
     # ---- host-array forms (the dictionary chains, the introgression model) ---------------
     def vanloan(self, Q: np.ndarray, t: float, masks: Dict[Omega, np.ndarray],

@@ -65,16 +65,19 @@ class StateSpace:
         return len(self.states)
 
     def rate_matrix(self, coal: float, rho: float) -> np.ndarray:
-        """Q[from, to] = coal or rho; Q[i, i] = -sum of row i (trans_mat.py:487-508)."""
+        """Q[from, to] = coal or rho; Q[i, i] = -sum of row i (trans_mat.py:487-508), the row
+        sum accumulated left to right like the reference's loop (np.cumsum is sequential)."""
         n = self.n
+        idx = self.__dict__.get("_tr_idx")
+        if idx is None:
+            tr = np.asarray(self.transitions, dtype=np.int64).reshape(-1, 3)
+            idx = (tr[:, 0], tr[:, 1], tr[:, 2] == 2)
+            object.__setattr__(self, "_tr_idx", idx)
+        f, t, is_rho = idx
         Q = np.zeros((n, n), dtype=np.float64)
-        for f, t, kind in self.transitions:
-            Q[f, t] = rho if kind == 2 else coal
-        for i in range(n):
-            acc = 0.0
-            for v in Q[i].tolist():  # sequential, diagonal still 0
-                acc += v
-            Q[i, i] = -acc
+        Q[f, t] = np.where(is_rho, rho, coal)
+        d = np.arange(n)
+        Q[d, d] = -np.cumsum(Q, axis=1)[:, -1]
         return Q
 
 
