@@ -284,14 +284,6 @@ bool post_split_path(int n, itr_plan_t p) {
          itr::mfma_geometry(n, itr::MODE_FWD_STORE).cfg < 0;
 }
 
-// The exponents of the matrix-core posterior's stored forward rows: after the rows in
-// d_alpha (reserve() sizes the buffer for both).
-int* post_ka(itr_plan_t p, int n) {
-  const int xa = itr::sweep_row_stride(n, itr::MODE_BWD);
-  const itr::MfmaGeometry g = itr::mfma_geometry(n, itr::MODE_BWD);
-  return reinterpret_cast<int*>(p->d_alpha + (size_t)p->total * std::max(xa, g.xr));
-}
-
 int reserve(itr_plan_t p, int n, bool vit, bool post) {
   const int xr = vit_stride(n);
   const int xa = itr::sweep_row_stride(n, itr::MODE_BWD);
@@ -309,9 +301,7 @@ int reserve(itr_plan_t p, int n, bool vit, bool post) {
   if (post) {
     const itr::MfmaGeometry g = itr::mfma_geometry(n, itr::MODE_BWD);
     const int stride = g.cfg >= 0 ? std::max(xa, g.xr) : xa;
-    // the matrix-core posterior also keeps one int exponent per stored row (post_ka)
-    need_rows = std::max(need_rows, (size_t)p->total * stride +
-                                        (g.cfg >= 0 ? ((size_t)p->total + 1) / 2 : 0));
+    need_rows = std::max(need_rows, (size_t)p->total * stride);
   }
   if (post && post_split_path(n, p) && (size_t)p->beta_rows * xa > p->beta_cap) {
     dev_free(p->d_beta);
@@ -409,7 +399,6 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   a.alpha = v.alpha;
   a.astride = g.xr;
   a.post = v.post;
-  if (!ll) a.ka = post_ka(p, m->n);
   a.prio_len = INT32_MAX;
   v.queue = p->d_queue + 3;
   v.prio_len = 0;  // every VALU task of the hybrid is a long block: raised wave priority
@@ -753,12 +742,10 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
       }
     }
   }
-  // Viterbi long set: blocks longer than 0.55 x the longest and >= 2,048 columns (a lone
-  // per-wave block steps ~2x slower than one in the 9-wave layout).  Measured on the chr10
-  // workload (scripts/gpu_lab4.sh, forward+Viterbi call): long fraction 0.45 / 0.55 / 0.65 ->
-  // 10.3 / 9.09 / 9.75 ms
+  // Viterbi long set: blocks longer than 0.45 x the longest and >= 2,048 columns (a lone
+  // per-wave block steps ~2x slower than one in the 9-wave layout)
   {
-    double lfrac = 0.55;
+    double lfrac = 0.45;
 #ifdef ITR_EXPERIMENT
     if (getenv("ITR_VIT_LONG_FRAC")) lfrac = atof(getenv("ITR_VIT_LONG_FRAC"));
 #endif
@@ -971,7 +958,7 @@ namespace {
 //
 // Work placement.  A block's sweep is a strictly sequential chain, so the
 // longest blocks need the lowest step latency and the bulk the highest throughput:
-//   * the longest blocks' Viterbi (longer than 0.55 x the longest, >= 2,048 columns): the
+//   * the longest blocks' Viterbi (longer than 0.45 x the longest, >= 2,048 columns): the
 //     9-wave VALU layout, one workgroup per CU, on `reserve` CUs (CU-masked stream lng);
 //   * with the forward: its latency-bound VALU tasks (halves of the longest blocks) on rf of
 //     those reserved CUs (lng2), and on the other CUs (blk) ONE persistent launch of

@@ -199,10 +199,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
           const double* x0tab = dir[gb] < 0 ? p.emit : p.init;
           x[gb] = (T[gb] > 0 && jv) ? x0tab[min(sym(gb, 0), 624) * n + j] : 0.0;
           if (jv) X[gb][0][r][j] = x[gb];
-          if (MODE == MODE_FWD_STORE && T[gb] > 0) {
-            p.alpha[c0[gb] * p.astride + j] = x[gb];
-            if (w == 0 && row_leader) p.ka[c0[gb]] = 0;
-          }
+          if (MODE == MODE_FWD_STORE && T[gb] > 0) p.alpha[c0[gb] * p.astride + j] = x[gb];
           xfin[gb] = x[gb];
           K[gb] = Kfin[gb] = 0;
 #pragma unroll
@@ -263,9 +260,8 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
                     xfin[gb] = x[gb];
                     Kfin[gb] = K[gb];
                   }
-                } else if (t < T[gb]) {
-                  p.alpha[(c0[gb] + t) * p.astride + j] = x[gb];
-                  if (w == 0 && row_leader) p.ka[c0[gb] + t] = K[gb];
+                } else {
+                  if (t < T[gb]) p.alpha[(c0[gb] + t) * p.astride + j] = x[gb];
                 }
                 if (jv) X[gb][buf ^ 1][r][j] = x[gb];
                 if (sub == 0 && (t0 & 7) == 0) {  // every 8th column: maxima for the rescale
@@ -309,57 +305,40 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
       } else {
         // ---------------- backward + posterior (optimizer.py:191-238)
         //   beta_{T-1} = 1;  beta_{t-1} = (beta_t * e_t) @ a   (vector @ a: the reference's form)
-        //   post_t = alpha_t * beta_t / P(obs)
-        // Step s handles column t = T - 1 - s of every block of the group.  The stored rows are
-        // alpha_t 2^-Ka(t) (p.ka), beta_t is kept as beta_t 2^-Kb; P(obs) = sum_j alpha_{T-1}
-        // = S0 2^Ka(T-1) is summed once, at the first step, so a step's posterior is
-        // alpha beta 2^(Ka(t) - Ka(T-1) + Kb) / S0 — elementwise, no cross-wave reduction per
-        // column (the reference normalises by the log-likelihood the same way).
+        //   post_t = alpha_t * beta_t / sum_j(alpha_t * beta_t)
+        // Step s handles column t = T - 1 - s of every block of the group.
         double bt[GB];
         double anxt[GB][TE];
-        int knxt[GB][TE];
-        double invS0[GB];
-        int KaT[GB], Kb[GB];
         // stored forward row of column T-1-s (unconditional load, see above: an empty row
         // reads row 0; padded target lanes read stored zeros)
         auto arow = [&](int gb, int s) -> double {
           const int tc = max(T[gb] - 1 - s, 0);
           return p.alpha[(T[gb] > 0 ? c0[gb] + tc : 0) * p.astride + j];
         };
-        auto krow = [&](int gb, int s) -> int {
-          const int tc = max(T[gb] - 1 - s, 0);
-          return p.ka[T[gb] > 0 ? c0[gb] + tc : 0];
-        };
 #pragma unroll
         for (int gb = 0; gb < GB; ++gb) {
           bt[gb] = (T[gb] > 0 && jv) ? 1.0 : 0.0;
-          invS0[gb] = 0.0;
-          KaT[gb] = Kb[gb] = 0;
 #pragma unroll
           for (int u = 0; u < TE; ++u) {
             enxt[gb][u] = emis(sym(gb, T[gb] - 1 - u));
             anxt[gb][u] = arow(gb, u);
-            knxt[gb][u] = krow(gb, u);
             snxt[gb][u] = sym(gb, T[gb] - 1 - (TE + u));
           }
         }
         wait_vmem_all();
         for (int s0 = 0; s0 < Tmax; s0 += TE) {
           double ecur[GB][TE], acur[GB][TE];
-          int kcur[GB][TE];
 #pragma unroll
           for (int gb = 0; gb < GB; ++gb) {
 #pragma unroll
             for (int u = 0; u < TE; ++u) {
               ecur[gb][u] = enxt[gb][u];
               acur[gb][u] = anxt[gb][u];
-              kcur[gb][u] = knxt[gb][u];
             }
 #pragma unroll
             for (int u = 0; u < TE; ++u) {
               enxt[gb][u] = emis(snxt[gb][u]);
               anxt[gb][u] = arow(gb, s0 + TE + u);
-              knxt[gb][u] = krow(gb, s0 + TE + u);
               snxt[gb][u] = sym(gb, T[gb] - 1 - (s0 + 2 * TE + u));
             }
           }
@@ -373,10 +352,8 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
               for (int gb = 0; gb < GB; ++gb) {
                 qv[gb] = acur[gb][sub] * bt[gb];  // padded states: 0 * 0
                 const double v = bt[gb] * ecur[gb][sub];
-                if (s == 0) {  // P(obs) of each block: sum_j alpha_{T-1} (beta_{T-1} = 1)
-                  const double ps = row16_sum(qv[gb]);
-                  if (row_leader) RS[gb][0][w][r] = ps;
-                }
+                const double ps = row16_sum(qv[gb]);
+                if (row_leader) RS[gb][buf][w][r] = ps;
                 if (sub == 0 && (s0 & 7) == 0) {
                   const double m = row16_max(v);
                   if (row_leader) RM[gb][w][r] = m;
@@ -386,26 +363,17 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
               lds_barrier();
 #pragma unroll
               for (int gb = 0; gb < GB; ++gb) {
-                if (s == 0) {
-                  double S = RS[gb][0][0][r];
+                double S = RS[gb][buf][0][r];
 #pragma unroll
-                  for (int v = 1; v < NT; ++v) S += RS[gb][0][v][r];
-                  invS0[gb] = 1.0 / S;
-                  KaT[gb] = kcur[gb][sub];
-                }
-                if (s < T[gb] && jv)
-                  p.post[(c0[gb] + (T[gb] - 1 - s)) * n + j] =
-                      qv[gb] * ldexp(invS0[gb], kcur[gb][sub] - KaT[gb] + Kb[gb]);
+                for (int v = 1; v < NT; ++v) S += RS[gb][buf][v][r];
+                const double rS = 1.0 / S;
+                if (s < T[gb] && jv) p.post[(c0[gb] + (T[gb] - 1 - s)) * n + j] = qv[gb] * rS;
                 double sc = 1.0;
                 if (sub == 0 && (s0 & 7) == 0) {
                   double M = RM[gb][0][r];
 #pragma unroll
                   for (int v = 1; v < NT; ++v) M = fmax(M, RM[gb][v][r]);
-                  if (M > 0.0 && M < INFINITY) {
-                    const int e = ilogb(M);
-                    sc = ldexp(1.0, -e);
-                    Kb[gb] += e;
-                  }
+                  if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
                 }
                 const double* xs = &X[gb][buf][ra][kk * NK];
                 double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;

@@ -91,8 +91,6 @@ struct MfmaArgs {
   double* alpha;                // forward rows, row stride astride (FWD_STORE out, BWD in)
   int64_t astride;
   double* post;                 // [total x n]                (MODE_BWD)
-  int* ka;                      // [total] power-of-two exponent of each stored forward row
-                                //   (FWD_STORE out, BWD in: the global normalisation)
   double* svec;                 // MODE_FWD_LL: split halves' vectors [slots x 2 x astride]
   int* sK;                      // MODE_FWD_LL: their power-of-two exponents [slots x 2]
   int prio_len;                 // groups at least this long run at raised wave priority
