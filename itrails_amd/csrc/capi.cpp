@@ -742,10 +742,12 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
       }
     }
   }
-  // Viterbi long set: blocks longer than 0.45 x the longest and >= 2,048 columns (a lone
-  // per-wave block steps ~2x slower than one in the 9-wave layout)
+  // Viterbi long set: blocks longer than 0.55 x the longest and >= 2,048 columns (a lone
+  // per-wave block steps ~2x slower than one in the 9-wave layout).  Measured on the chr10
+  // workload (scripts/gpu_lab4.sh, forward+Viterbi call): long fraction 0.45 / 0.55 / 0.65 ->
+  // 10.3 / 9.09 / 9.75 ms
   {
-    double lfrac = 0.45;
+    double lfrac = 0.55;
 #ifdef ITR_EXPERIMENT
     if (getenv("ITR_VIT_LONG_FRAC")) lfrac = atof(getenv("ITR_VIT_LONG_FRAC"));
 #endif
@@ -958,7 +960,7 @@ namespace {
 //
 // Work placement.  A block's sweep is a strictly sequential chain, so the
 // longest blocks need the lowest step latency and the bulk the highest throughput:
-//   * the longest blocks' Viterbi (longer than 0.45 x the longest, >= 2,048 columns): the
+//   * the longest blocks' Viterbi (longer than 0.55 x the longest, >= 2,048 columns): the
 //     9-wave VALU layout, one workgroup per CU, on `reserve` CUs (CU-masked stream lng);
 //   * with the forward: its latency-bound VALU tasks (halves of the longest blocks) on rf of
 //     those reserved CUs (lng2), and on the other CUs (blk) ONE persistent launch of
