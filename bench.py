@@ -180,8 +180,10 @@ def pmc_traffic(n, mode, tag_hint=""):
                     f"{os.path.basename(f)} (" + " + ".join(k for k, _ in parts) +
                     "): FETCH_SIZE+WRITE_SIZE per call, raw")
         for name, v in d.items():
-            if name.startswith("void itr::sweep_kernel<") and \
-                    name.endswith(f", {mode}>(itr::SweepArgs)") and \
+            hyb = re.search(r"hybrid_sweep_kernel<\d+, \d+, \d+, (\d+),", name)
+            if ((name.startswith("void itr::sweep_kernel<") and
+                 name.endswith(f", {mode}>(itr::SweepArgs)")) or
+                    (hyb and int(hyb.group(1)) == mode)) and \
                     v.get("n_states", 70) == n and "hbm_bytes_raw" in v:
                 return round(v["hbm_bytes_raw"]), (
                     f"{os.path.basename(f)} ({name}): FETCH_SIZE+WRITE_SIZE per launch, raw")

@@ -24,7 +24,16 @@ def main():
     d_obs = torch.from_numpy(W["obs"].astype(np.int16)).cuda()
     ll = torch.empty(plan.nblocks, dtype=torch.float64, device="cuda")
     path = torch.empty(plan.total, dtype=torch.uint8, device="cuda")
+    post = None
+    if "post" in which:  # config 3: the (7,7) model's posterior over the same 10 Mbp
+        a7, b7, pi7, _ = load_model(7)
+        W7 = make_workload("chr10", a7, b7, pi7, 0, 1, 2000.0)
+        m7, p7 = hmm.Model(a7, b7, pi7), hmm.Plan(W7["off"])
+        o7 = torch.from_numpy(W7["obs"].astype(np.int16)).cuda()
+        post = torch.empty((p7.total, a7.shape[0]), dtype=torch.float64, device="cuda")
     for _ in range(reps):
+        if "post" in which:
+            hmm.posterior_device(m7, p7, o7, out=post)
         if "fwd" in which:
             hmm.forward_loglik_device(model, plan, d_obs, out=ll)
         if "vit" in which:
