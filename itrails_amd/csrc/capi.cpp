@@ -114,18 +114,22 @@ struct Partition {
 // its streams, so a worker thread's exit returns its hardware-queue streams)
 struct Partitions {
   std::deque<Partition> v;
-  void release() {
+  static void destroy(Partition& x) {  // waits for the streams' work
     int dev = 0;
     const bool have_dev = hipGetDevice(&dev) == hipSuccess;
-    for (auto& x : v) {
-      (void)hipSetDevice(x.device);
-      for (hipStream_t* q : {&x.lng, &x.lng2, &x.blk})
-        if (*q) (void)hipStreamDestroy(*q);
-      for (hipEvent_t* e : {&x.fork, &x.jl, &x.jl2, &x.jb})
-        if (*e) (void)hipEventDestroy(*e);
-    }
-    v.clear();
+    (void)hipSetDevice(x.device);
+    for (hipStream_t* q : {&x.lng, &x.lng2, &x.blk})
+      if (*q) {
+        (void)hipStreamSynchronize(*q);
+        (void)hipStreamDestroy(*q);
+      }
+    for (hipEvent_t* e : {&x.fork, &x.jl, &x.jl2, &x.jb})
+      if (*e) (void)hipEventDestroy(*e);
     if (have_dev) (void)hipSetDevice(dev);
+  }
+  void release() {
+    for (auto& x : v) destroy(x);
+    v.clear();
   }
   ~Partitions() { release(); }
 };
@@ -139,6 +143,10 @@ int partition(int reserve, Partition** out) {
       *out = &x;
       return 0;
     }
+  if (g_parts.v.size() >= 4) {  // a few partitions per thread (each holds 3 hardware queues)
+    Partitions::destroy(g_parts.v.front());
+    g_parts.v.pop_front();
+  }
   const int cus = cu_count();
   std::vector<uint32_t> ml((cus + 31) / 32, 0u), mb((cus + 31) / 32, 0u);
   std::vector<char> in(cus, 0);
@@ -969,7 +977,9 @@ namespace {
 //   * without the mixed launch (other state counts): the forward's matrix-core groups, then
 //     the per-wave Viterbi on blk.
 // When the long blocks would keep the reserved CUs busy longer than the rest keeps the
-// others (few, equally long blocks), every block goes to the 9-wave layout on all CUs.
+// others (few, equally long blocks), every block goes to the 9-wave layout: with the
+// forward and at most 3/4 as many blocks as CUs, one CU per block and the forward on the
+// remaining CUs at the same time; otherwise on all CUs after the forward.
 int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
                  hipStream_t st, double* fwd_loglik) {
   if (int e = reserve(p, m->n, true, false)) return e;
@@ -1001,8 +1011,25 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     const double t_bulk = (double)(p->total - p->vit_long_cols) * kVitWaveCuNs / (cus - reserve_cus);
     if (t_long > 1.1 * std::max(t_bulk, (double)p->sorted_len[0] * kVitLoneNs)) wave = false;
   }
-  if (!wave && fwd_loglik)  // no overlap: the forward sweep first, on the caller's stream
+  // Few blocks, all long (e.g. 100 blocks of 100 kbp): one CU per block for the 9-wave
+  // Viterbi sweep and the forward sweep beside it on the remaining CUs (at least a quarter
+  // of the chip), instead of one after the other
+  const bool few = !wave && fwd_loglik && p->nblocks <= cus - cus / 4;
+  if (few) {
+    Partition* pt = nullptr;
+    if (int e = partition((int)p->nblocks, &pt)) return e;
+    HIP_TRY(hipEventRecord(pt->fork, st));
+    HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
+    HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
+    if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, p->nblocks)) return e;
+    if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, pt->blk)) return e;
+    HIP_TRY(hipEventRecord(pt->jl, pt->lng));
+    HIP_TRY(hipEventRecord(pt->jb, pt->blk));
+    HIP_TRY(hipStreamWaitEvent(st, pt->jl, 0));
+    HIP_TRY(hipStreamWaitEvent(st, pt->jb, 0));
+  } else if (!wave && fwd_loglik) {  // no overlap: the forward sweep first, on st
     if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, st)) return e;
+  }
   if (wave) {
     itr::VitArgs w{};
     w.n = m->n;
@@ -1123,7 +1150,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     if (split_fwd)  // log P of the split blocks from their two halves
       HIP_TRY(itr::launch_fwd_split_combine(m->n, gf.xr, (int)p->nhsplit, p->d_hsplit_blk,
                                             p->d_svec, p->d_sK, fwd_loglik, st));
-  } else {
+  } else if (!few) {
     if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
   }
   both.reset();

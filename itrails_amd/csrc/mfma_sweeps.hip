@@ -80,7 +80,7 @@ template <int NT, int NK, int GB>
 struct MLds {
   static constexpr int KP = 4 * NK;
   static constexpr size_t x_off = 0;                                   // X[GB][2][4][KP]
-  static constexpr size_t rs_off = x_off + (size_t)GB * 2 * 4 * KP * 8;  // RS[GB][2][NT][4]
+  static constexpr size_t rs_off = x_off + (size_t)GB * 2 * 4 * KP * 8;  // RS[GB][2][4][NT]
   static constexpr size_t rm_off = rs_off + (size_t)GB * 2 * NT * 4 * 8; // RM[GB][NT][4]
   static constexpr size_t kf_off = rm_off + (size_t)GB * NT * 4 * 8;     // KF[GB][4]
   static constexpr size_t bytes = kf_off + (size_t)GB * 4 * 4;
@@ -95,7 +95,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
   constexpr int TB = 64 * NT;
   using LD = MLds<NT, NK, GB>;
   auto X = reinterpret_cast<double (*)[2][4][KP]>(smem + LD::x_off);    // published vectors
-  auto RS = reinterpret_cast<double (*)[2][NT][4]>(smem + LD::rs_off);  // row partial sums
+  auto RS = reinterpret_cast<double (*)[2][4][NT]>(smem + LD::rs_off);  // row partial sums
   auto RM = reinterpret_cast<double (*)[NT][4]>(smem + LD::rm_off);     // row maxima
   auto KF = reinterpret_cast<int (*)[4]>(smem + LD::kf_off);
 
@@ -285,7 +285,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
             }
             // log P = log(sum_j x_j) + K ln 2   (optimizer.py:160-162)
             const double s = row16_sum(xfin[gb]);
-            if (row_leader) RS[gb][0][w][r] = s;
+            if (row_leader) RS[gb][0][r][w] = s;
             if (w == 0 && row_leader) KF[gb][r] = Kfin[gb];
           }
           lds_barrier();
@@ -296,7 +296,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
             if (id >= 0 && p.tasks[3 * id + 1] == 0) {
               const int b2 = p.tasks[3 * id];
               double S = 0.0;
-              for (int v = 0; v < NT; ++v) S += RS[gb][0][v][rr];
+              for (int v = 0; v < NT; ++v) S += RS[gb][0][rr][v];
               const int T2 = (int)(p.off[b2 + 1] - p.off[b2]);
               p.loglik[b2] = T2 > 0 ? log(S) + (double)KF[gb][rr] * LN2 : 0.0;
             }
@@ -353,7 +353,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
                 qv[gb] = acur[gb][sub] * bt[gb];  // padded states: 0 * 0
                 const double v = bt[gb] * ecur[gb][sub];
                 const double ps = row16_sum(qv[gb]);
-                if (row_leader) RS[gb][buf][w][r] = ps;
+                if (row_leader) RS[gb][buf][r][w] = ps;
                 if (sub == 0 && (s0 & 7) == 0) {
                   const double m = row16_max(v);
                   if (row_leader) RM[gb][w][r] = m;
@@ -363,18 +363,8 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
               lds_barrier();
 #pragma unroll
               for (int gb = 0; gb < GB; ++gb) {
-                double S = RS[gb][buf][0][r];
-#pragma unroll
-                for (int v = 1; v < NT; ++v) S += RS[gb][buf][v][r];
-                const double rS = 1.0 / S;
-                if (s < T[gb] && jv) p.post[(c0[gb] + (T[gb] - 1 - s)) * n + j] = qv[gb] * rS;
-                double sc = 1.0;
-                if (sub == 0 && (s0 & 7) == 0) {
-                  double M = RM[gb][0][r];
-#pragma unroll
-                  for (int v = 1; v < NT; ++v) M = fmax(M, RM[gb][v][r]);
-                  if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
-                }
+                // the matrix product first; the column's normalisation (a log-depth tree over
+                // the NT wave partials) and the rescale maximum while it runs
                 const double* xs = &X[gb][buf][ra][kk * NK];
                 double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
 #pragma unroll
@@ -383,6 +373,15 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
                   if (q + 1 < NK) a1 = mfma4(xs[q + 1], B[q + 1], a1);
                   if (q + 2 < NK) a2 = mfma4(xs[q + 2], B[q + 2], a2);
                   if (q + 3 < NK) a3 = mfma4(xs[q + 3], B[q + 3], a3);
+                }
+                const double rS = recip_nr(tree_sum<NT>(&RS[gb][buf][r][0]));
+                if (s < T[gb] && jv) p.post[(c0[gb] + (T[gb] - 1 - s)) * n + j] = qv[gb] * rS;
+                double sc = 1.0;
+                if (sub == 0 && (s0 & 7) == 0) {
+                  double M = RM[gb][0][r];
+#pragma unroll
+                  for (int v = 1; v < NT; ++v) M = fmax(M, RM[gb][v][r]);
+                  if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
                 }
                 bt[gb] = ((a0 + a1) + (a2 + a3)) * sc;
               }

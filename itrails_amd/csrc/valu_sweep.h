@@ -132,6 +132,43 @@ __device__ __forceinline__ double row_sum(double v) {
   return v + dpp_f64<DPP_R8>(v);
 }
 
+// Sum / maximum over the four 16-lane rows of a wave whose lanes hold their row's value:
+// wave-uniform, from four lane reads (no LDS round trip)
+__device__ __forceinline__ double lane_f64(double v, int lane) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
+                          __builtin_amdgcn_readlane(__double2loint(v), lane));
+}
+__device__ __forceinline__ double rows4_sum(double v) {
+  return (lane_f64(v, 0) + lane_f64(v, 16)) + (lane_f64(v, 32) + lane_f64(v, 48));
+}
+__device__ __forceinline__ double rows4_max(double v) {
+  return fmax(fmax(lane_f64(v, 0), lane_f64(v, 16)), fmax(lane_f64(v, 32), lane_f64(v, 48)));
+}
+// 1 / s by the hardware reciprocal and one Newton step (a few ulps; the posterior's
+// normalisation, whose bar is 1e-8 relative, instead of the ten-instruction IEEE division on
+// the backward sweep's step)
+__device__ __forceinline__ double recip_nr(double s) {
+  const double r = __builtin_amdgcn_rcp(s);
+  return fma(fma(-s, r, 1.0), r, r);
+}
+// pairwise sum / maximum of N consecutive values (independent LDS reads, log-depth chain)
+template <int N>
+__device__ __forceinline__ double tree_sum(const double* a) {
+  if constexpr (N == 1) {
+    return a[0];
+  } else {
+    return tree_sum<N / 2>(a) + tree_sum<N - N / 2>(a + N / 2);
+  }
+}
+template <int N>
+__device__ __forceinline__ double tree_max(const double* a) {
+  if constexpr (N == 1) {
+    return a[0];
+  } else {
+    return fmax(tree_max<N / 2>(a), tree_max<N - N / 2>(a + N / 2));
+  }
+}
+
 // Stores through a wave-uniform base as a buffer resource (base and byte bound in SGPRs):
 // the per-lane part is one 32-bit byte offset instead of a 64-bit address pair, and a lane
 // whose offset is kOffNone (past the bound) stores nothing, without a branch.
@@ -297,9 +334,6 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
   const int l = tid & 63;
   const int q = l & (QL - 1);
   const int jl = l / QL;
-  const int row16 = w * 4 + (l >> 4);  // 16-lane row of the workgroup (0..4W-1)
-  constexpr int NROW = 4 * W;
-  const bool row_leader = (l & 15) == 0;
 
   double* X = reinterpret_cast<double*>(smem);  // [2][XS+64]    published vectors + a
                                                 //               per-lane write sink
@@ -452,12 +486,12 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
 #pragma unroll
               for (int r = 0; r < RJN; ++r) Xb[jx[r]] = x[r];
               const bool rescale = (sub & 7) == 1;
-              if (rescale) {  // row maxima of x_{t-1} (padded states hold 0)
+              if (rescale) {  // the wave's maximum of x_{t-1} (padded states hold 0)
                 double mx = x[0];
 #pragma unroll
                 for (int r = 1; r < RJN; ++r) mx = fmax(mx, x[r]);
-                mx = row_max<QL>(mx);
-                if (row_leader) RED[128 + buf * 64 + row16] = mx;
+                mx = rows4_max(row_max<QL>(mx));
+                if (l == 0) RED[128 + buf * 64 + w] = mx;
               }
               // emission factors of column t: staged at the start of this tile, so (except
               // on the tile's first step, which commits them) readable before the barrier
@@ -493,9 +527,7 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
                 for (int r = 0; r < RJN; ++r) acc[k % NCH][r] = fma(xi, m[k][r], acc[k % NCH][r]);
               }
               if (rescale) {  // fold 2^-e into the emission factor (off the FMA chain)
-                double M = RED[128 + buf * 64];
-#pragma unroll
-                for (int v = 1; v < NROW; ++v) M = fmax(M, RED[128 + buf * 64 + v]);
+                const double M = tree_max<W>(RED + 128 + buf * 64);
                 const bool ok = M > 0.0 && M < INFINITY;
                 const int e = ok ? ilogb(M) : 0;
                 const double sc = ldexp(1.0, -e);
@@ -560,8 +592,26 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
         double bt[RJN];
 #pragma unroll
         for (int r = 0; r < RJN; ++r) bt[r] = jv[r] ? 1.0 : 0.0;
-        double* sink = p.sink + l;  // padded states store here (never read)
+        // posterior rows through a buffer resource on the block's rows: lane offset = its
+        // state (padded states: out of range, nothing stored), row offset in a scalar register
+        // (blocks whose rows span 4 GiB or more store through 64-bit addresses instead)
+        const bool wide = (int64_t)T * n * 8 >= (int64_t)kOffNone;
+        const __amdgpu_buffer_rsrc_t rpost =
+            buf_rsrc(p.post && !wide ? p.post + c0 * n : p.sink,
+                     p.post && !wide ? (uint32_t)((int64_t)T * n * 8) : 0u);
+        uint32_t voff[RJN];
+#pragma unroll
+        for (int r = 0; r < RJN; ++r) voff[r] = jv[r] ? (uint32_t)jr[r] * 8u : kOffNone;
         wait_vmem_all();
+        // the staged emission / forward values of a step are read from LDS one step ahead
+        // (after the previous step's barrier): the published vector v = beta * e needs them
+        // before the barrier, where a read issued on the spot would stall the wave
+        double ecur[RJN], acur[RJN];
+#pragma unroll
+        for (int r = 0; r < RJN; ++r) {
+          ecur[r] = staged(EST, 0, jr[r]);
+          acur[r] = need_alpha ? staged(AST, 0, jr[r]) : 0.0;
+        }
         for (int s0 = 0; s0 < T; s0 += TE) {
 #pragma unroll
           for (int sub = 0; sub < TE; ++sub) {
@@ -573,53 +623,39 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
               double qv[RJN], v[RJN], ps = 0.0;
 #pragma unroll
               for (int r = 0; r < RJN; ++r) {
-                v[r] = bt[r] * staged(EST, s, jr[r]);
+                v[r] = bt[r] * ecur[r];
                 Xb[jx[r]] = v[r];
               }
+              // per-wave partials (the wave's four rows combined by lane reads): after the
+              // barrier only W values are combined, by a log-depth tree, and after the
+              // matrix product has been issued (a 4W-long chain of dependent LDS reads and
+              // adds before it cost more than the product itself at N = 133)
               if (need_alpha) {
 #pragma unroll
                 for (int r = 0; r < RJN; ++r) {
-                  qv[r] = staged(AST, s, jr[r]) * bt[r];  // padded states: 0 * 0
+                  qv[r] = acur[r] * bt[r];  // padded states: 0 * 0
                   ps += qv[r];
                 }
-                ps = row_sum<QL>(ps);  // the row's target-state groups
-                if (row_leader) RED[buf * 64 + row16] = ps;
+                ps = rows4_sum(row_sum<QL>(ps));  // the wave's target states
+                if (l == 0) RED[buf * 64 + w] = ps;
               }
               const bool rescale = (sub & 7) == 0;
               if (rescale) {
                 double mx = v[0];
 #pragma unroll
                 for (int r = 1; r < RJN; ++r) mx = fmax(mx, v[r]);
-                mx = row_max<QL>(mx);
-                if (row_leader) RED[128 + buf * 64 + row16] = mx;
+                mx = rows4_max(row_max<QL>(mx));
+                if (l == 0) RED[128 + buf * 64 + w] = mx;
               }
               if (sub == 0) ot.advance(s, tid);
               if (sub == TE - 1) stage_commit(s + 1);
               lds_barrier();
               if (sub == TE - 1) stage_issue(s + 1);
-              if (p.beta) {
-                // concurrent split (launch_post_split): this block's forward rows are being
-                // written by another workgroup, so store beta_t for post_combine instead
-                const int64_t brow = (p.beta_off[blk] + t) * XR;
+              // next step's staged values (its tile was committed before this barrier)
 #pragma unroll
-                for (int r = 0; r < RJN; ++r) p.beta[brow + jr[r]] = bt[r];
-              } else {
-                double S = 0.0;
-#pragma unroll
-                for (int u = 0; u < NROW; ++u) S += RED[buf * 64 + u];
-                const double rS = 1.0 / S;
-#pragma unroll
-                for (int r = 0; r < RJN; ++r) {
-                  double* dst = jv[r] ? p.post + (c0 + t) * n + jr[r] : sink;
-                  *dst = qv[r] * rS;
-                }
-              }
-              double sc = 1.0;
-              if (rescale) {
-                double M = RED[128 + buf * 64];
-#pragma unroll
-                for (int u = 1; u < NROW; ++u) M = fmax(M, RED[128 + buf * 64 + u]);
-                if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
+              for (int r = 0; r < RJN; ++r) {
+                ecur[r] = staged(EST, s + 1, jr[r]);
+                if (need_alpha) acur[r] = staged(AST, s + 1, jr[r]);
               }
               const double* xs = Xb + q * IQS;
               double acc[NCH][RJN];
@@ -632,6 +668,29 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
                 const double xi = xs[k];
 #pragma unroll
                 for (int r = 0; r < RJN; ++r) acc[k % NCH][r] = fma(xi, m[k][r], acc[k % NCH][r]);
+              }
+              if (p.beta) {
+                // concurrent split (launch_post_split): this block's forward rows are being
+                // written by another workgroup, so store beta_t for post_combine instead
+                const int64_t brow = (p.beta_off[blk] + t) * XR;
+#pragma unroll
+                for (int r = 0; r < RJN; ++r) p.beta[brow + jr[r]] = bt[r];
+              } else {
+                const double rS = recip_nr(tree_sum<W>(RED + buf * 64));
+                if (!wide) {
+                  const uint32_t row = (uint32_t)t * (uint32_t)n * 8u;
+#pragma unroll
+                  for (int r = 0; r < RJN; ++r) buf_store_f64(rpost, voff[r], row, qv[r] * rS);
+                } else {
+#pragma unroll
+                  for (int r = 0; r < RJN; ++r)
+                    if (jv[r]) p.post[(c0 + t) * n + jr[r]] = qv[r] * rS;
+                }
+              }
+              double sc = 1.0;
+              if (rescale) {
+                const double M = tree_max<W>(RED + 128 + buf * 64);
+                if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
               }
               double sum[RJN];
 #pragma unroll
