@@ -11,7 +11,7 @@
 // three-stage DPP all-reduce and runs the per-column tail redundantly, against 153 useful
 // adds/maxes.  Here one wavefront decodes a whole block on its own (no workgroup barrier):
 //
-//   lane l = 8 g + q holds sources i in [IQ q, IQ q + IQ) x targets j in [IQ g, IQ g + IQ)
+//   lane l = 8 q + g holds sources i in [IQ q, IQ q + IQ) x targets j in [IQ g, IQ g + IQ)
 //   of log a in VGPRs (loaded once per wave), forms the IQ partial maxima
 //   z_j = max_i (omega_i + log a_ij) over its sources (IQ^2 adds, IQ^2 - IQ maxes), writes
 //   them to the wave's partial table P[j][q] in LDS, and then finalises ONE target j = l
@@ -160,7 +160,10 @@ __device__ __forceinline__ void vit_wave_task(const VitArgs& p, double* wl, int 
   using C = WaveVit<IQ>;
   constexpr int XRW = C::XRW, NB = C::NB, IQS = C::IQS, XN = C::XN, PS = C::PS, HT = C::HT,
                 NI = C::NI, EB = C::EB;
-  const int l = lane_id_fresh(), q = l & 7, g = l >> 3;
+  // q high, g low: a 16-lane store group of the partial writes (ds_write_b64, banks mod 32)
+  // then covers 8 target rows x 2 chunks at distinct banks (q low: 2 rows x 8 chunks, 2-way
+  // on 4 banks; measured 41 of 141 LDS cycles per column as SQ_LDS_BANK_CONFLICT)
+  const int l = lane_id_fresh(), q = l >> 3, g = l & 7;
   const int n = p.n;
   const int64_t xr = p.xr;
   double* X = wl;

@@ -64,8 +64,12 @@ def main():
         ref = O.forward_loglik(t, obs, off)
         hmm.forward_loglik_device(model, plan, d_obs, out=ll)
         err_f = np.max(np.abs(ll.cpu().numpy() / ref - 1))
+        ref_path = O.viterbi(t, obs, off)
+        hmm.viterbi_device(model, plan, d_obs, out=path)
+        print(f"{args.tag} check: viterbi paths equal {np.array_equal(path.cpu().numpy(), ref_path)}",
+              flush=True)
         hmm.forward_viterbi_device(model, plan, d_obs, out_ll=ll, out_path=path)
-        ok_p = np.array_equal(path.cpu().numpy(), O.viterbi(t, obs, off))
+        ok_p = np.array_equal(path.cpu().numpy(), ref_path)
         err = np.max(np.abs(ll.cpu().numpy() / ref - 1))
         print(f"{args.tag} check: forward max rel err {err_f:.2e}; combined: paths equal {ok_p}, "
               f"loglik max rel err {err:.2e}", flush=True)
