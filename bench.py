@@ -190,6 +190,37 @@ def pmc_traffic(n, mode, tag_hint=""):
     return None, "no PMC summary under profiles/ for this kernel"
 
 
+def pmc_rates(n):
+    """Issue and matrix-core counters of the sweep kernels from the latest committed
+    rocprofv3 --pmc summary (scripts/gpu_r3g.sh -> scripts/pmc_summary.py): per kernel the
+    share of SIMD-cycles with the MFMA pipe busy (SQ_VALU_MFMA_BUSY_CYCLES) and with FP64 VALU
+    work issued (SQ_INSTS_VALU x 4 cycles), normalised to the SIMDs of the CUs the launch ran
+    on, plus the waves' waitcnt share (SQ_WAIT_ANY / SQ_WAVE_CYCLES)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))
+    for f in reversed(files):
+        d = json.load(open(f))
+        out = {}
+        for name, v in d.items():
+            if v.get("n_states", 70) != n or "mfma_util" not in v or \
+                    not ("sweep_kernel" in name or "wave_" in name):
+                continue
+            # CU share of the launch: the combined call's bulk kernels run on 192 of 256 CUs
+            # (the others are reserved for the long blocks), the long-block sweep on 40
+            share = 1.0
+            if "wave_mixed_kernel" in name or "wave_vit_kernel" in name:
+                share = 192 / 256
+            elif name.startswith("void itr::sweep_kernel<") and name.endswith(", 3>(itr::SweepArgs)"):
+                share = 40 / 256
+            short = re.sub(r"\(itr::.*$", "", name.replace("void itr::", "")
+                           .replace("(anonymous namespace)::", ""))
+            out[short] = {"mfma_busy": round(v["mfma_util"] / share, 3),
+                          "valu_busy": round(v.get("valu_busy", 0.0) / share, 3),
+                          "wait_share": v.get("wait_share")}
+        if out:
+            return out, os.path.basename(f)
+    return None, None
+
+
 # ---------------------------------------------------------------------------------------
 # CPU restatement: checker + baseline (oracle/, test infrastructure; never the product)
 # ---------------------------------------------------------------------------------------
@@ -543,6 +574,7 @@ def main():
             ideal_ms = pair_ops * cols_local / (fma_peak * 1e12) * 1e3
         achieved = pair_ops * cols_local / (dom_ms * 1e-3) / 1e12 if dom_ms else 0.0
         traffic, traffic_note = pmc_traffic(n, dom_mode)
+        rates, rates_src = pmc_rates(n)
         cpu = None
         if opt_mode:
             f = os.path.join(ROOT, "tests", "golden",
@@ -631,6 +663,7 @@ def main():
                          "step_ideal_ms": round(ideal_ms, 4),
                          "step_frac": round(ideal_ms / step_ms, 5) if not opt_mode else None},
             "cpu_baseline": cpu,
+            **({"counters": {"source": rates_src, "kernels": rates}} if rates else {}),
             **({"build_ms": round(float(np.mean(build_ms)), 1)} if opt_mode else {}),
             **({"per_rank_step_ms": per_rank_ms, "allreduce_ms": xchg_ms,
                 "allreduce_bytes": int(d_ll_global.numel() * 8)} if world > 1 else {}),

@@ -105,6 +105,7 @@ int cu_count() {
 // queue with another and serialises against it (measured: 10 -> 12.5 ms per forward+Viterbi).
 struct Partition {
   int device = -1, reserve = 0;
+  bool masked = true;
   hipStream_t lng = nullptr, lng2 = nullptr;  // the reserved CUs
   hipStream_t blk = nullptr;                   // the other CUs
   hipEvent_t fork = nullptr, jl = nullptr, jl2 = nullptr, jb = nullptr;
@@ -135,11 +136,11 @@ struct Partitions {
 };
 thread_local Partitions g_parts;
 
-int partition(int reserve, Partition** out) {
+int partition(int reserve, Partition** out, bool masked = true) {
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   for (auto& x : g_parts.v)
-    if (x.device == dev && x.reserve == reserve) {
+    if (x.device == dev && x.reserve == reserve && x.masked == masked) {
       *out = &x;
       return 0;
     }
@@ -149,12 +150,34 @@ int partition(int reserve, Partition** out) {
   }
   const int cus = cu_count();
   std::vector<uint32_t> ml((cus + 31) / 32, 0u), mb((cus + 31) / 32, 0u);
+  // Logical CU-mask bit b addresses XCC b % X, CU b / X of that XCC, and an XCC left with no
+  // bit set is not masked at all (measured on MI355X, X = 8: scripts/micro/cumask2.hip,
+  // profiles/r3r_cumask.txt).  So the reserved CUs are chosen per XCC — reserve / X of each
+  // XCC's cus / X, spread over its CU indices — and each XCC keeps at least one CU on both
+  // sides of the partition.
+  const int X = (cus % 8 == 0) ? 8 : 1, L = cus / X;
   std::vector<char> in(cus, 0);
-  for (int k = 0; k < reserve; ++k) in[(int)((int64_t)k * cus / reserve)] = 1;
+  int mode = 0;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_MASK_MODE")) mode = atoi(getenv("ITR_MASK_MODE"));
+#endif
+  if (mode == 1) {  // round-2 pattern: every (cus / reserve)-th logical bit
+    for (int k = 0; k < reserve; ++k) in[(int)((int64_t)k * cus / reserve)] = 1;
+  } else {
+    for (int x = 0; x < X; ++x) {
+      const int r = std::min(L - 1, reserve / X + (x < reserve % X ? 1 : 0));
+      for (int k = 0; k < r; ++k) in[(int)(((2 * k + 1) * (int64_t)L / (2 * r)) * X + x)] = 1;
+    }
+  }
   for (int c = 0; c < cus; ++c) (in[c] ? ml : mb)[c / 32] |= 1u << (c % 32);
+  if (mode == 2 || !masked) {  // no masks
+    std::fill(ml.begin(), ml.end(), 0xFFFFFFFFu);
+    std::fill(mb.begin(), mb.end(), 0xFFFFFFFFu);
+  }
   Partition x;
   x.device = dev;
   x.reserve = reserve;
+  x.masked = masked;
   HIP_TRY(hipExtStreamCreateWithCUMask(&x.lng, (uint32_t)ml.size() * 32, ml.data()));
   HIP_TRY(hipExtStreamCreateWithCUMask(&x.lng2, (uint32_t)ml.size() * 32, ml.data()));
   HIP_TRY(hipExtStreamCreateWithCUMask(&x.blk, (uint32_t)mb.size() * 32, mb.data()));
@@ -750,12 +773,12 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
       }
     }
   }
-  // Viterbi long set: blocks longer than 0.55 x the longest and >= 2,048 columns (a lone
+  // Viterbi long set: blocks longer than 0.45 x the longest and >= 2,048 columns (a lone
   // per-wave block steps ~2x slower than one in the 9-wave layout).  Measured on the chr10
-  // workload (scripts/gpu_lab4.sh, forward+Viterbi call): long fraction 0.45 / 0.55 / 0.65 ->
-  // 10.3 / 9.09 / 9.75 ms
+  // workload, forward+Viterbi call, with the per-XCC CU partition (profiles/r3t_partition.txt):
+  // long fraction 0.45 + 72 reserved CUs 8.74-8.79 ms vs 0.55 + 64 9.34-9.85 ms
   {
-    double lfrac = 0.55;
+    double lfrac = 0.45;
 #ifdef ITR_EXPERIMENT
     if (getenv("ITR_VIT_LONG_FRAC")) lfrac = atof(getenv("ITR_VIT_LONG_FRAC"));
 #endif
@@ -996,7 +1019,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   const itr::WaveVitGeometry wv = itr::wave_vit_geometry(m->n);
   bool wave = wv.iq > 0 && m->LEW && m->xrw == wv.xr;
   const int cus = cu_count();
-  int reserve_cus = cus / 4;
+  int reserve_cus = (9 * cus) / 32;  // 72 of 256 (profiles/r3t_partition.txt)
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_VIT_RESERVE")) reserve_cus = atoi(getenv("ITR_VIT_RESERVE"));
 #endif
@@ -1016,8 +1039,11 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   // of the chip), instead of one after the other
   const bool few = !wave && fwd_loglik && p->nblocks <= cus - cus / 4;
   if (few) {
+    // unmasked streams: with one CU per Viterbi block masked off, the forward's halves
+    // queue for the remaining CUs; unmasked, the dispatcher places a forward workgroup beside
+    // a Viterbi block (100 x 100 kbp: 62 -> 36.5 ms, profiles/r3t_partition.txt)
     Partition* pt = nullptr;
-    if (int e = partition((int)p->nblocks, &pt)) return e;
+    if (int e = partition((int)p->nblocks, &pt, false)) return e;
     HIP_TRY(hipEventRecord(pt->fork, st));
     HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
     HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
@@ -1097,7 +1123,10 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       }
     }
     hipStream_t sb = pt ? pt->blk : st;
-    const int ocus = cus - (pt ? reserve_cus : 0);  // CUs of the sb launches
+    int ocus = cus - (pt ? reserve_cus : 0);  // CUs of the sb launches
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_MIX_CUS")) ocus = atoi(getenv("ITR_MIX_CUS"));
+#endif
     if (mixed) {
       // forward groups (the hybrid plan's matrix-core tasks) and the per-wave Viterbi blocks
       // from one queue ordered by expected duration (plan: mix list)

@@ -423,17 +423,26 @@ __device__ __forceinline__ void fwd_wave_task(const WaveMfmaArgs& p, double* wl,
   }
   wave_lds_sync();
   auto sym_at = [&](int r, int s) -> int { return SYM[((s >> 6) & 1) * 256 + r * 64 + (s & 63)]; };
-  // emission rows of half-tile h -> EST[h & 1]: element (u, r, j) at (u 4 + r) ER + j
+  // emission rows of half-tile h -> EST[h & 1]: element (u, r, j) at (u 4 + r) ER + j.
+  // Piece 64 i + l of a half-tile is (column u, row r, targets 2c, 2c + 1): lane constants,
+  // packed once per task as (r 64 + u) | 2c << 8 (the half-tile's symbols start at an even
+  // column, so column u of it is SYM entry base + r 64 + u of one 64-column chunk)
+  static_assert(HT == 2 && 2 * ER < (1 << 23), "piece packing");
+  int pk[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int pc = 64 * i + l;
+    const int u = pc / (2 * ER), rem = pc % (2 * ER), r = rem / (ER / 2), c = rem % (ER / 2);
+    pk[i] = pc < PIECES ? ((r * 64 + u) | (2 * c) << 8) : -1;
+  }
   auto stage_issue = [&](int h) {
     double* d = EST + (h & 1) * EB;
+    const int s = h * HT;
+    const int base = ((s >> 6) & 1) * 256 + (s & 63);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int pc = 64 * i + l;
       const double* src = p.ef;
-      if (pc < PIECES) {
-        const int u = pc / (2 * ER), rem = pc % (2 * ER), r = rem / (ER / 2), c = rem % (ER / 2);
-        src += (int64_t)sym_at(r, h * HT + u) * ER + 2 * c;
-      }
+      if (pk[i] >= 0) src += (int64_t)SYM[base + (pk[i] & 255)] * ER + (pk[i] >> 8);
       __builtin_amdgcn_global_load_lds(
           src, (__attribute__((address_space(3))) void*)(d + 128 * i), 16, 0, 0);
     }

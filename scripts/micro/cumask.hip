@@ -43,6 +43,17 @@ int main() {
   mk("first100", [](int i) { return i < 100; });
   mk("even", [](int i) { return i % 2 == 0; });
   mk("mod8_0", [](int i) { return i % 8 == 0; });
+  for (int b = 0; b < 16; ++b) {  // single logical bits: which physical CU is bit b?
+    static char nm[16][16];
+    snprintf(nm[b], 16, "bit%d", b * 17 % 256);
+    const int bb = b * 17 % 256;
+    mk(nm[b], [bb](int i) { return i == bb; });
+  }
+  for (int b = 0; b < 8; ++b) {
+    static char nm2[8][16];
+    snprintf(nm2[b], 16, "bit%d", b);
+    mk(nm2[b], [b](int i) { return i == b; });
+  }
   for (auto& M : masks) {
     hipStream_t s;
     hipExtStreamCreateWithCUMask(&s, (uint32_t)M.m.size() * 32, M.m.data());
@@ -58,7 +69,12 @@ int main() {
       cu.insert(((uint64_t)x << 16) | (se << 8) | (sh << 4) | cuid);
       xcc.insert(x);
     }
-    printf("%-10s distinct CUs %zu, XCCs %zu\n", M.name, cu.size(), xcc.size());
+    printf("%-10s distinct CUs %zu, XCCs %zu", M.name, cu.size(), xcc.size());
+    if (cu.size() <= 2)
+      for (uint64_t c : cu)
+        printf("  [xcc %u se %u sh %u cu %u]", (unsigned)(c >> 16), (unsigned)((c >> 8) & 0xff),
+               (unsigned)((c >> 4) & 0xf), (unsigned)(c & 0xf));
+    printf("\n");
     hipStreamDestroy(s);
   }
   return 0;
