@@ -257,6 +257,10 @@ struct itr_plan {
   // Viterbi blocks, < 0 = forward groups of groups_ll, by expected duration; tasks at least
   // mix_prio_* long run at raised wave priority
   int64_t vit_nlong = 0, vit_long_cols = 0, nmix = 0;
+  // CU partition (plan_partition): reserved CUs for the long blocks' Viterbi and for the
+  // forward's VALU halves; wave_ok = false when the long work cannot fit half the chip
+  int vit_reserve = 0, fwd_reserve = 0;
+  bool wave_ok = true;
   int32_t* d_mix = nullptr;
   int mix_prio_fwd = INT32_MAX, mix_prio_vit = INT32_MAX;
   int64_t nutasks = 0, ngroups_ll = 0, nhsplit = 0;
@@ -299,11 +303,74 @@ int vit_stride(int n) {
   return wv.iq > 0 ? wv.xr : itr::sweep_row_stride(n, itr::MODE_VIT);
 }
 
-// Measured per-column costs of the two Viterbi layouts at N = 70: a block
-// alone on its CU in the 9-wave layout steps in ~325 ns; the per-wave sweep on a loaded CU
-// costs ~114 CU-ns per column.  They decide whether the CU partition pays (viterbi_impl).
-constexpr double kVitLoneNs = 325e-9;
-constexpr double kVitWaveCuNs = 114e-9;
+// Per-column costs of the sweep layouts of the (5,5) model (N = 65..72, the only state counts
+// with the per-wave layouts), measured on MI355X (profiles/r3l_*, r3u_*):
+//   kVitLone    a Viterbi block alone on its CU, 9-wave VALU layout           325 ns / column
+//   kVitWaveLat a per-wave Viterbi block's step under full load (latency)      800 ns / column
+//   kVitWaveCu  per-wave Viterbi throughput                                    114 CU-ns / column
+//   kFwdWaveCu  per-wave matrix-core forward throughput                         55 CU-ns / column
+//   kFwdValu    a forward VALU half alone on its CU                            370 ns / column
+constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kVitWaveCu = 114e-9,
+                 kFwdWaveCu = 55e-9, kFwdValu = 370e-9;
+
+// Bins of capacity `cap` (first fit, items longest first): the CUs a set of sequential tasks
+// needs to finish within cap
+int ffd_bins(const std::vector<int64_t>& items, double cap) {
+  std::vector<double> bins;
+  for (int64_t t : items) {
+    bool placed = false;
+    for (double& b : bins)
+      if (b + (double)t <= cap) {
+        b += (double)t;
+        placed = true;
+        break;
+      }
+    if (!placed) bins.push_back((double)t);
+  }
+  return (int)bins.size();
+}
+
+// The forward+Viterbi CU partition of a plan (viterbi_impl).  Expected makespan T: the whole
+// workload at the bulk layouts' throughput over every CU, or the longest block alone on the
+// 9-wave layout, whichever is longer.  A block whose per-wave Viterbi step latency would
+// exceed T joins the long set; the long set gets the CUs it needs to finish within T at the
+// lone-block step time, the forward's VALU halves (`ulen`) the CUs they need at theirs,
+// rounded up to whole XCC sets (8 CUs: one per XCC).  The reserved CUs join the bulk queue
+// when their long work is done, so a generous reservation costs little.
+void plan_partition(itr_plan_t p, const std::vector<int64_t>& ulen, int cus) {
+  const int64_t nblocks = p->nblocks;
+  const double tmax = nblocks ? (double)p->sorted_len[0] : 0.0;
+  double wlat = kVitWaveLat;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_WAVE_LAT")) wlat = atof(getenv("ITR_WAVE_LAT"));
+#endif
+  const double T = std::max((double)p->total * (kVitWaveCu + kFwdWaveCu) / cus, tmax * kVitLone);
+  int64_t k = 0, cols = 0;
+  std::vector<int64_t> lng;
+  while (k < nblocks && p->sorted_len[k] >= 2048 && (double)p->sorted_len[k] * wlat > T) {
+    lng.push_back(p->sorted_len[k]);
+    cols += p->sorted_len[k++];
+  }
+  p->vit_nlong = k;
+  p->vit_long_cols = cols;
+  const int rv = ffd_bins(lng, T / kVitLone);
+  std::vector<int64_t> halves(ulen);
+  std::sort(halves.begin(), halves.end(), std::greater<int64_t>());
+  const int rf = ffd_bins(halves, T / kFwdValu);
+  const int X = (cus % 8 == 0) ? 8 : 1;
+  auto whole = [&](int r) { return r > 0 ? (r + X - 1) / X * X : 0; };
+  p->fwd_reserve = rf;
+  p->vit_reserve = whole(rv + rf) - rf;
+  p->wave_ok = rv + rf <= cus / 2;
+  if (getenv("ITR_VERBOSE"))
+    fprintf(stderr, "[itr] partition: T %.3f ms, long %lld blocks (%lld cols), rv %d rf %d (%zu halves)%s\n",
+            T * 1e3, (long long)k, (long long)cols, p->vit_reserve, rf, halves.size(),
+            p->wave_ok ? "" : ", no wave layout");
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_VIT_RESERVE")) p->vit_reserve = atoi(getenv("ITR_VIT_RESERVE"));
+  if (getenv("ITR_FWD_RESERVE")) p->fwd_reserve = atoi(getenv("ITR_FWD_RESERVE"));
+#endif
+}
 
 // The posterior's concurrent split (launch_post_split): only on the VALU-only posterior
 // (no matrix-core form at this state count) and only where the blocks are few
@@ -536,7 +603,12 @@ int itr_model_create(int n, const double* a, const double* la, const double* E,
     m->xrw = w;
   }
   const itr::WaveMfmaGeometry wf = itr::wave_mfma_geometry(n);
-  if (wf.cfg >= 0) {
+#ifdef ITR_EXPERIMENT
+  const bool need_ef = wf.cfg >= 0;  // ITR_WAVE_FWD: the per-wave forward at every size
+#else
+  const bool need_ef = wf.mixed;     // the mixed launch's forward groups
+#endif
+  if (need_ef) {
     const int w = wf.er;
     std::vector<double> ef((size_t)(ITR_NOBS + 1) * w, 0.0);
     for (int o = 0; o < ITR_NOBS; ++o)
@@ -773,21 +845,8 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
       }
     }
   }
-  // Viterbi long set: blocks longer than 0.45 x the longest and >= 2,048 columns (a lone
-  // per-wave block steps ~2x slower than one in the 9-wave layout).  Measured on the chr10
-  // workload, forward+Viterbi call, with the per-XCC CU partition (profiles/r3t_partition.txt):
-  // long fraction 0.45 + 72 reserved CUs 8.74-8.79 ms vs 0.55 + 64 9.34-9.85 ms
-  {
-    double lfrac = 0.45;
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_VIT_LONG_FRAC")) lfrac = atof(getenv("ITR_VIT_LONG_FRAC"));
-#endif
-    int64_t k = 0, cols = 0;
-    while (k < nblocks && p->sorted_len[k] >= 2048 && (double)p->sorted_len[k] > lfrac * (double)tmax)
-      cols += p->sorted_len[k++];
-    p->vit_nlong = k;
-    p->vit_long_cols = cols;
-  }
+  // Viterbi long set and the CU partition of the forward+Viterbi call
+  plan_partition(p, ulen, cu_count());
   // The mixed queue: forward groups (steps = their longest member) and the remaining Viterbi
   // blocks merged by expected duration, longest first.  Measured per-column step times under
   // full load at N = 70: a forward group ~0.92 us, a per-wave Viterbi block ~0.64 us.
@@ -1019,21 +1078,8 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   const itr::WaveVitGeometry wv = itr::wave_vit_geometry(m->n);
   bool wave = wv.iq > 0 && m->LEW && m->xrw == wv.xr;
   const int cus = cu_count();
-  int reserve_cus = (9 * cus) / 32;  // 72 of 256 (profiles/r3t_partition.txt)
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_VIT_RESERVE")) reserve_cus = atoi(getenv("ITR_VIT_RESERVE"));
-#endif
-  reserve_cus = std::max(1, std::min(reserve_cus, cus - 1));
+  if (wave && !p->wave_ok) wave = false;  // the long work would need more than half the CUs
   const int64_t nlong = wave ? p->vit_nlong : 0;
-  if (wave) {
-    // Keep the partition when the reserved CUs finish the long blocks no later than the
-    // other CUs finish the rest (or than the longest block alone), by the measured per-column
-    // costs (plan: vit_lone_ns for a block alone on its CU in the 9-wave layout,
-    // vit_wave_cu_ns CU-ns per column of the per-wave sweep on a loaded CU)
-    const double t_long = (double)p->vit_long_cols * kVitLoneNs / reserve_cus;
-    const double t_bulk = (double)(p->total - p->vit_long_cols) * kVitWaveCuNs / (cus - reserve_cus);
-    if (t_long > 1.1 * std::max(t_bulk, (double)p->sorted_len[0] * kVitLoneNs)) wave = false;
-  }
   // Few blocks, all long (e.g. 100 blocks of 100 kbp): one CU per block for the 9-wave
   // Viterbi sweep and the forward sweep beside it on the remaining CUs (at least a quarter
   // of the chip), instead of one after the other
@@ -1080,10 +1126,10 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     Partition* pt = nullptr;
     const itr::MfmaGeometry gf = itr::mfma_geometry(m->n, itr::MODE_FWD_LL);
     const itr::WaveMfmaGeometry wf = itr::wave_mfma_geometry(m->n);
-    // the forward's VALU tasks (halves of the longest blocks) on rf reserved CUs; they must
-    // not outnumber the reserved CUs
-    const bool split_fwd = fwd_loglik && nlong > 0 && gf.cfg >= 0 && p->ngroups_ll > 0 &&
-                           p->nutasks > 0 && p->nutasks < reserve_cus;
+    // the forward's VALU tasks (halves of the longest blocks) on rf reserved CUs, the long
+    // blocks' Viterbi on rv others (plan_partition)
+    const bool split_fwd = fwd_loglik && gf.cfg >= 0 && p->ngroups_ll > 0 && p->nutasks > 0 &&
+                           p->fwd_reserve > 0;
     bool mixed = split_fwd && wf.mixed && m->EF && p->nmix > 0;
 #ifdef ITR_EXPERIMENT
     if (getenv("ITR_NO_MIXED")) mixed = false;
@@ -1098,32 +1144,39 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     af.nblocks = p->nutasks;
     af.svec = p->d_svec;
     af.sK = p->d_sK;
-    int64_t rf = 0;  // reserved CUs for the forward's VALU tasks
+    const int64_t rf = split_fwd ? p->fwd_reserve : 0;
+    const int64_t rv = nlong > 0 ? std::max(1, p->vit_reserve) : 0;
+    // whole XCC sets: a mask that leaves an XCC without a reserved CU does not mask it at all
+    const int X = (cus % 8 == 0) ? 8 : 1;
+    const int reserve_cus = (int)std::min<int64_t>((rv + rf + X - 1) / X * X, cus / 2);
     if (split_fwd) {
-      rf = std::min<int64_t>(p->nutasks, 3 * reserve_cus / 8);
-#ifdef ITR_EXPERIMENT
-      if (getenv("ITR_FWD_RESERVE"))
-        rf = std::min<int64_t>(atoi(getenv("ITR_FWD_RESERVE")), reserve_cus - 1);
-#endif
       HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
       HIP_TRY(hipMemsetAsync(p->d_queue + 8, 0, 2 * sizeof(int), st));  // the idle loops' counters
     }
-    if (nlong > 0) {
+    // before the fork: the bulk queue is shared with the reserved CUs' late launch
+    HIP_TRY(hipMemsetAsync(mixed ? p->d_queue + 12 : w.queue, 0, sizeof(int), st));
+    if (reserve_cus > 0) {
       if (int e = partition(reserve_cus, &pt)) return e;
       HIP_TRY(hipEventRecord(pt->fork, st));
       HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
       HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
-      a.nblocks = nlong;
-      if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, reserve_cus - rf)) return e;
+      if (nlong > 0) {
+        a.nblocks = nlong;
+        if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, rv)) return e;
+      }
       if (split_fwd) {
         HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
         if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, pt->lng2, nullptr, true, false,
                                rf, false))
           return e;
+        // the reserved CUs' late launch (below) waits for the VALU halves too: a bulk
+        // workgroup beside a running long task would slow the critical path
+        HIP_TRY(hipEventRecord(pt->jl2, pt->lng2));
+        HIP_TRY(hipStreamWaitEvent(pt->lng, pt->jl2, 0));
       }
     }
     hipStream_t sb = pt ? pt->blk : st;
-    int ocus = cus - (pt ? reserve_cus : 0);  // CUs of the sb launches
+    int ocus = cus - reserve_cus;  // CUs of the sb launches
 #ifdef ITR_EXPERIMENT
     if (getenv("ITR_MIX_CUS")) ocus = atoi(getenv("ITR_MIX_CUS"));
 #endif
@@ -1149,9 +1202,11 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       f.prio_len = p->mix_prio_fwd;
       w.prio_len = p->mix_prio_vit;
       const int64_t grid = std::min<int64_t>((int64_t)wf.mixed_per_cu * ocus, (p->nmix + 3) / 4);
-      HIP_TRY(hipMemsetAsync(p->d_queue + 12, 0, sizeof(int), sb));
       HIP_TRY(itr::launch_wave_mixed(wf, (int)grid, w, f, p->d_mix, (int)p->nmix,
                                      p->d_queue + 12, sb));
+      if (pt)  // the reserved CUs join the bulk queue when their long work is done
+        HIP_TRY(itr::launch_wave_mixed(wf, wf.mixed_per_cu * reserve_cus, w, f, p->d_mix,
+                                       (int)p->nmix, p->d_queue + 12, pt->lng));
     } else {
       if (split_fwd) {
         if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, sb, nullptr, false, true,
@@ -1162,8 +1217,9 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       }
       if (w.nblocks > 0) {  // the per-wave sweep: after the forward's matrix-core groups
         const int64_t grid = std::min<int64_t>((int64_t)wv.per_cu * ocus, (w.nblocks + 3) / 4);
-        HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), sb));
         HIP_TRY(itr::launch_wave_vit(wv, (int)grid, w, sb));
+        if (pt)  // the reserved CUs join when their long work is done
+          HIP_TRY(itr::launch_wave_vit(wv, wv.per_cu * reserve_cus, w, pt->lng));
       }
     }
     if (pt) {

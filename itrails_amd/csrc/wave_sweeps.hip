@@ -33,6 +33,7 @@ __global__ void __launch_bounds__(64 * kWaves, 2) wave_vit_kernel(VitArgs p) {
   }
 }
 
+#ifdef ITR_EXPERIMENT  // the forward alone on the per-wave layout: experiment library only
 template <int NT, int NK>
 __global__ void __launch_bounds__(64 * kWaves, 2) wave_fwd_kernel(WaveMfmaArgs p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -43,6 +44,7 @@ __global__ void __launch_bounds__(64 * kWaves, 2) wave_fwd_kernel(WaveMfmaArgs p
     fwd_wave_task<NT, NK>(p, wl, gi);
   }
 }
+#endif
 
 // One queue of both kinds: entry e >= 0 = the Viterbi block e, e < 0 = forward group -e - 1.
 template <int IQ, int NT, int NK>
@@ -82,7 +84,7 @@ struct WCfg {
 constexpr WCfg kWCfgs[] = {{33, 48, 3, 12}, {49, 64, 4, 16}, {65, 72, 5, 18}};
 
 template <int NT, int NK>
-size_t wf_lds() {
+[[maybe_unused]] size_t wf_lds() {
   return (size_t)kWaves * WF<NT, NK>::WL * sizeof(double);
 }
 
@@ -119,11 +121,13 @@ WaveMfmaGeometry wave_mfma_geometry(int n) {
   if (g.cfg < 0) return g;
   g.block = 64 * kWaves;
   g.er = 16 * kWCfgs[g.cfg].nt;
+#ifdef ITR_EXPERIMENT
   switch (g.cfg) {
     case 0: g.lds = wf_lds<3, 12>(); g.per_cu = occupancy(wave_fwd_kernel<3, 12>, g.lds); break;
     case 1: g.lds = wf_lds<4, 16>(); g.per_cu = occupancy(wave_fwd_kernel<4, 16>, g.lds); break;
     case 2: g.lds = wf_lds<5, 18>(); g.per_cu = occupancy(wave_fwd_kernel<5, 18>, g.lds); break;
   }
+#endif
   // the mixed launch (Viterbi blocks + forward groups) exists for the (5,5) model's sizes
   g.mixed = (n > 64 && n <= 72) && g.cfg == 2;
   if (g.mixed) {
@@ -135,6 +139,10 @@ WaveMfmaGeometry wave_mfma_geometry(int n) {
 
 hipError_t launch_wave_mfma(const WaveMfmaGeometry& g, int grid, const WaveMfmaArgs& p,
                             hipStream_t st) {
+#ifndef ITR_EXPERIMENT
+  (void)g, (void)grid, (void)p, (void)st;
+  return hipErrorInvalidValue;
+#else
   switch (g.cfg) {
     case 0: hipLaunchKernelGGL((wave_fwd_kernel<3, 12>), dim3(grid), dim3(g.block), g.lds, st, p); break;
     case 1: hipLaunchKernelGGL((wave_fwd_kernel<4, 16>), dim3(grid), dim3(g.block), g.lds, st, p); break;
@@ -142,6 +150,7 @@ hipError_t launch_wave_mfma(const WaveMfmaGeometry& g, int grid, const WaveMfmaA
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+#endif
 }
 
 hipError_t launch_wave_mixed(const WaveMfmaGeometry& g, int grid, const VitArgs& v,
