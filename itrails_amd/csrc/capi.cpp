@@ -104,7 +104,7 @@ int cu_count() {
 // 4 hardware queues a process gets by default (GPU_MAX_HW_QUEUES); a fifth stream shares a
 // queue with another and serialises against it (measured: 10 -> 12.5 ms per forward+Viterbi).
 struct Partition {
-  int device = -1, reserve = 0;
+  int device = -1, reserve = 0, reserve2 = 0;
   bool masked = true;
   hipStream_t lng = nullptr, lng2 = nullptr;  // the reserved CUs
   hipStream_t blk = nullptr;                   // the other CUs
@@ -136,11 +136,12 @@ struct Partitions {
 };
 thread_local Partitions g_parts;
 
-int partition(int reserve, Partition** out, bool masked = true) {
+// lng on `reserve` CUs, lng2 on `reserve2` others (0: lng2 on lng's CUs), blk on the rest
+int partition(int reserve, int reserve2, Partition** out, bool masked = true) {
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   for (auto& x : g_parts.v)
-    if (x.device == dev && x.reserve == reserve && x.masked == masked) {
+    if (x.device == dev && x.reserve == reserve && x.reserve2 == reserve2 && x.masked == masked) {
       *out = &x;
       return 0;
     }
@@ -149,14 +150,15 @@ int partition(int reserve, Partition** out, bool masked = true) {
     g_parts.v.pop_front();
   }
   const int cus = cu_count();
-  std::vector<uint32_t> ml((cus + 31) / 32, 0u), mb((cus + 31) / 32, 0u);
+  const int nw = (cus + 31) / 32;
+  std::vector<uint32_t> ml(nw, 0u), ml2(nw, 0u), mb(nw, 0u);
   // Logical CU-mask bit b addresses XCC b % X, CU b / X of that XCC, and an XCC left with no
   // bit set is not masked at all (measured on MI355X, X = 8: scripts/micro/cumask2.hip,
   // profiles/r3r_cumask.txt).  So the reserved CUs are chosen per XCC — reserve / X of each
-  // XCC's cus / X, spread over its CU indices — and each XCC keeps at least one CU on both
-  // sides of the partition.
+  // XCC's cus / X, spread over its CU indices — and each XCC keeps at least one CU on every
+  // side of the partition.
   const int X = (cus % 8 == 0) ? 8 : 1, L = cus / X;
-  std::vector<char> in(cus, 0);
+  std::vector<char> in(cus, 0);  // 1: lng, 2: lng2
   int mode = 0;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_MASK_MODE")) mode = atoi(getenv("ITR_MASK_MODE"));
@@ -165,21 +167,35 @@ int partition(int reserve, Partition** out, bool masked = true) {
     for (int k = 0; k < reserve; ++k) in[(int)((int64_t)k * cus / reserve)] = 1;
   } else {
     for (int x = 0; x < X; ++x) {
-      const int r = std::min(L - 1, reserve / X + (x < reserve % X ? 1 : 0));
-      for (int k = 0; k < r; ++k) in[(int)(((2 * k + 1) * (int64_t)L / (2 * r)) * X + x)] = 1;
+      const int r1 = reserve / X + (x < reserve % X ? 1 : 0);
+      const int r2 = reserve2 / X + (x < reserve2 % X ? 1 : 0);
+      const int r = std::min(L - 1, r1 + r2);
+      const int q2 = std::min(r2, r);
+      for (int k = 0; k < r; ++k) {
+        const int c = (int)(((2 * k + 1) * (int64_t)L / (2 * r)) * X + x);
+        in[c] = 1;
+        // every (r / q2)-th reserved position of the XCC goes to lng2
+        for (int j = 0; j < q2; ++j)
+          if (k == (int)((2 * j + 1) * (int64_t)r / (2 * q2))) in[c] = 2;
+      }
     }
   }
-  for (int c = 0; c < cus; ++c) (in[c] ? ml : mb)[c / 32] |= 1u << (c % 32);
+  for (int c = 0; c < cus; ++c)
+    (in[c] == 1 ? ml : in[c] == 2 ? ml2 : mb)[c / 32] |= 1u << (c % 32);
+  if (reserve <= 0) std::fill(ml.begin(), ml.end(), 0xFFFFFFFFu);  // (lng unused)
+  if (reserve2 <= 0) ml2 = ml;
   if (mode == 2 || !masked) {  // no masks
     std::fill(ml.begin(), ml.end(), 0xFFFFFFFFu);
+    std::fill(ml2.begin(), ml2.end(), 0xFFFFFFFFu);
     std::fill(mb.begin(), mb.end(), 0xFFFFFFFFu);
   }
   Partition x;
   x.device = dev;
   x.reserve = reserve;
+  x.reserve2 = reserve2;
   x.masked = masked;
   HIP_TRY(hipExtStreamCreateWithCUMask(&x.lng, (uint32_t)ml.size() * 32, ml.data()));
-  HIP_TRY(hipExtStreamCreateWithCUMask(&x.lng2, (uint32_t)ml.size() * 32, ml.data()));
+  HIP_TRY(hipExtStreamCreateWithCUMask(&x.lng2, (uint32_t)ml2.size() * 32, ml2.data()));
   HIP_TRY(hipExtStreamCreateWithCUMask(&x.blk, (uint32_t)mb.size() * 32, mb.data()));
   HIP_TRY(hipEventCreateWithFlags(&x.fork, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&x.jl, hipEventDisableTiming));
@@ -357,10 +373,8 @@ void plan_partition(itr_plan_t p, const std::vector<int64_t>& ulen, int cus) {
   std::vector<int64_t> halves(ulen);
   std::sort(halves.begin(), halves.end(), std::greater<int64_t>());
   const int rf = ffd_bins(halves, T / kFwdValu);
-  const int X = (cus % 8 == 0) ? 8 : 1;
-  auto whole = [&](int r) { return r > 0 ? (r + X - 1) / X * X : 0; };
-  p->fwd_reserve = rf;
-  p->vit_reserve = whole(rv + rf) - rf;
+  p->fwd_reserve = rf;  // (viterbi_impl rounds both up to whole XCC sets)
+  p->vit_reserve = rv;
   p->wave_ok = rv + rf <= cus / 2;
   if (getenv("ITR_VERBOSE"))
     fprintf(stderr, "[itr] partition: T %.3f ms, long %lld blocks (%lld cols), rv %d rf %d (%zu halves)%s\n",
@@ -1089,7 +1103,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     // queue for the remaining CUs; unmasked, the dispatcher places a forward workgroup beside
     // a Viterbi block (100 x 100 kbp: 62 -> 36.5 ms, profiles/r3t_partition.txt)
     Partition* pt = nullptr;
-    if (int e = partition((int)p->nblocks, &pt, false)) return e;
+    if (int e = partition((int)p->nblocks, 0, &pt, false)) return e;
     HIP_TRY(hipEventRecord(pt->fork, st));
     HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
     HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
@@ -1148,7 +1162,9 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     const int64_t rv = nlong > 0 ? std::max(1, p->vit_reserve) : 0;
     // whole XCC sets: a mask that leaves an XCC without a reserved CU does not mask it at all
     const int X = (cus % 8 == 0) ? 8 : 1;
-    const int reserve_cus = (int)std::min<int64_t>((rv + rf + X - 1) / X * X, cus / 2);
+    const int rvr = (int)std::min<int64_t>((rv + X - 1) / X * X, cus / 2);
+    const int rfr = (int)std::min<int64_t>((rf + X - 1) / X * X, cus / 4);
+    const int reserve_cus = rvr + rfr;
     if (split_fwd) {
       HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
       HIP_TRY(hipMemsetAsync(p->d_queue + 8, 0, 2 * sizeof(int), st));  // the idle loops' counters
@@ -1156,23 +1172,22 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     // before the fork: the bulk queue is shared with the reserved CUs' late launch
     HIP_TRY(hipMemsetAsync(mixed ? p->d_queue + 12 : w.queue, 0, sizeof(int), st));
     if (reserve_cus > 0) {
-      if (int e = partition(reserve_cus, &pt)) return e;
+      // the long blocks' Viterbi on lng (rvr CUs), the forward's VALU halves on lng2 (rfr
+      // others): separate masks, so each set joins the bulk queue as soon as its own long
+      // work is done without a bulk workgroup landing beside a running long task
+      if (int e = partition(rvr, rfr, &pt)) return e;
       HIP_TRY(hipEventRecord(pt->fork, st));
       HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
       HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
       if (nlong > 0) {
         a.nblocks = nlong;
-        if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, rv)) return e;
+        if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, rvr)) return e;
       }
       if (split_fwd) {
         HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
         if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, pt->lng2, nullptr, true, false,
-                               rf, false))
+                               rfr, false))
           return e;
-        // the reserved CUs' late launch (below) waits for the VALU halves too: a bulk
-        // workgroup beside a running long task would slow the critical path
-        HIP_TRY(hipEventRecord(pt->jl2, pt->lng2));
-        HIP_TRY(hipStreamWaitEvent(pt->lng, pt->jl2, 0));
       }
     }
     hipStream_t sb = pt ? pt->blk : st;
@@ -1204,9 +1219,14 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       const int64_t grid = std::min<int64_t>((int64_t)wf.mixed_per_cu * ocus, (p->nmix + 3) / 4);
       HIP_TRY(itr::launch_wave_mixed(wf, (int)grid, w, f, p->d_mix, (int)p->nmix,
                                      p->d_queue + 12, sb));
-      if (pt)  // the reserved CUs join the bulk queue when their long work is done
-        HIP_TRY(itr::launch_wave_mixed(wf, wf.mixed_per_cu * reserve_cus, w, f, p->d_mix,
-                                       (int)p->nmix, p->d_queue + 12, pt->lng));
+      if (pt) {  // the reserved CUs join the bulk queue when their long work is done
+        if (rvr > 0)
+          HIP_TRY(itr::launch_wave_mixed(wf, wf.mixed_per_cu * rvr, w, f, p->d_mix,
+                                         (int)p->nmix, p->d_queue + 12, pt->lng));
+        if (rfr > 0)
+          HIP_TRY(itr::launch_wave_mixed(wf, wf.mixed_per_cu * rfr, w, f, p->d_mix,
+                                         (int)p->nmix, p->d_queue + 12, pt->lng2));
+      }
     } else {
       if (split_fwd) {
         if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, sb, nullptr, false, true,
@@ -1218,8 +1238,10 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       if (w.nblocks > 0) {  // the per-wave sweep: after the forward's matrix-core groups
         const int64_t grid = std::min<int64_t>((int64_t)wv.per_cu * ocus, (w.nblocks + 3) / 4);
         HIP_TRY(itr::launch_wave_vit(wv, (int)grid, w, sb));
-        if (pt)  // the reserved CUs join when their long work is done
-          HIP_TRY(itr::launch_wave_vit(wv, wv.per_cu * reserve_cus, w, pt->lng));
+        if (pt && rvr > 0)  // the reserved CUs join when their long work is done
+          HIP_TRY(itr::launch_wave_vit(wv, wv.per_cu * rvr, w, pt->lng));
+        if (pt && rfr > 0)
+          HIP_TRY(itr::launch_wave_vit(wv, wv.per_cu * rfr, w, pt->lng2));
       }
     }
     if (pt) {
