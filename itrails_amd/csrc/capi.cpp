@@ -145,10 +145,10 @@ int partition(int reserve, int reserve2, Partition** out, bool masked = true) {
       *out = &x;
       return 0;
     }
-  if (g_parts.v.size() >= 4) {  // a few partitions per thread (each holds 3 hardware queues)
-    Partitions::destroy(g_parts.v.front());
-    g_parts.v.pop_front();
-  }
+  // one partition per thread: its three streams plus the caller's are the process's 4
+  // hardware queues (GPU_MAX_HW_QUEUES); a second partition's streams would share queues with
+  // the first's and serialise behind them
+  g_parts.release();
   const int cus = cu_count();
   const int nw = (cus + 31) / 32;
   std::vector<uint32_t> ml(nw, 0u), ml2(nw, 0u), mb(nw, 0u);
@@ -166,22 +166,31 @@ int partition(int reserve, int reserve2, Partition** out, bool masked = true) {
   if (mode == 1) {  // round-2 pattern: every (cus / reserve)-th logical bit
     for (int k = 0; k < reserve; ++k) in[(int)((int64_t)k * cus / reserve)] = 1;
   } else {
+    // within an XCC, CU index k belongs to shader engine k % 4 (cumask2.hip: local k ->
+    // se k % 4); the dispatcher deals a launch's workgroups to the shader engines in turn, so
+    // each set takes the same number of CUs from every engine (a one-workgroup-per-CU launch
+    // then finds a CU in whichever engine its workgroup is dealt to)
+    const int S = (L % 4 == 0) ? 4 : 1, E = L / S;  // engines per XCC, CUs per engine
     for (int x = 0; x < X; ++x) {
       const int r1 = reserve / X + (x < reserve % X ? 1 : 0);
       const int r2 = reserve2 / X + (x < reserve2 % X ? 1 : 0);
-      const int r = std::min(L - 1, r1 + r2);
-      const int q2 = std::min(r2, r);
-      for (int k = 0; k < r; ++k) {
-        const int c = (int)(((2 * k + 1) * (int64_t)L / (2 * r)) * X + x);
-        in[c] = 1;
-        // every (r / q2)-th reserved position of the XCC goes to lng2
-        for (int j = 0; j < q2; ++j)
-          if (k == (int)((2 * j + 1) * (int64_t)r / (2 * q2))) in[c] = 2;
+      for (int set = 1; set <= 2; ++set) {
+        const int r = set == 1 ? r1 : r2;
+        for (int k = 0; k < r; ++k) {
+          const int se = k % S;
+          // the j-th CU of this set in engine se, after the CUs of the sets before it
+          const int j = k / S + (set == 2 ? r1 / S + (se < r1 % S ? 1 : 0) : 0);
+          if (j >= E - 1) continue;  // every engine keeps a CU for the bulk
+          in[(int)((int64_t)(j * S + se) * X + x)] = (char)set;
+        }
       }
     }
   }
   for (int c = 0; c < cus; ++c)
     (in[c] == 1 ? ml : in[c] == 2 ? ml2 : mb)[c / 32] |= 1u << (c % 32);
+  if (mode == 3)  // the bulk may share the long Viterbi blocks' CUs (one workgroup beside each)
+    for (int c = 0; c < cus; ++c)
+      if (in[c] == 1) mb[c / 32] |= 1u << (c % 32);
   if (reserve <= 0) std::fill(ml.begin(), ml.end(), 0xFFFFFFFFu);  // (lng unused)
   if (reserve2 <= 0) ml2 = ml;
   if (mode == 2 || !masked) {  // no masks
@@ -323,11 +332,11 @@ int vit_stride(int n) {
 // with the per-wave layouts), measured on MI355X (profiles/r3l_*, r3u_*):
 //   kVitLone    a Viterbi block alone on its CU, 9-wave VALU layout           325 ns / column
 //   kVitWaveLat a per-wave Viterbi block's step under full load (latency)      800 ns / column
-//   kVitWaveCu  per-wave Viterbi throughput                                    114 CU-ns / column
-//   kFwdWaveCu  per-wave matrix-core forward throughput                         55 CU-ns / column
+//   kBulkCu     forward + Viterbi of a column in the mixed per-wave launch     180 CU-ns / column
+//               (calibrated on chr10: 0.15 / 0.165 / 0.18 / 0.195 us -> forward+Viterbi call
+//               8.52 / 8.49 / 8.29-8.69 / 8.41-8.56 ms, profiles/r3ab5_partition.txt)
 //   kFwdValu    a forward VALU half alone on its CU                            370 ns / column
-constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kVitWaveCu = 114e-9,
-                 kFwdWaveCu = 55e-9, kFwdValu = 370e-9;
+constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kBulkCu = 180e-9, kFwdValu = 370e-9;
 
 // Bins of capacity `cap` (first fit, items longest first): the CUs a set of sequential tasks
 // needs to finish within cap
@@ -356,11 +365,12 @@ int ffd_bins(const std::vector<int64_t>& items, double cap) {
 void plan_partition(itr_plan_t p, const std::vector<int64_t>& ulen, int cus) {
   const int64_t nblocks = p->nblocks;
   const double tmax = nblocks ? (double)p->sorted_len[0] : 0.0;
-  double wlat = kVitWaveLat;
+  double wlat = kVitWaveLat, bulk = kBulkCu;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_WAVE_LAT")) wlat = atof(getenv("ITR_WAVE_LAT"));
+  if (getenv("ITR_BULK_CU")) bulk = atof(getenv("ITR_BULK_CU"));
 #endif
-  const double T = std::max((double)p->total * (kVitWaveCu + kFwdWaveCu) / cus, tmax * kVitLone);
+  const double T = std::max((double)p->total * bulk / cus, tmax * kVitLone);
   int64_t k = 0, cols = 0;
   std::vector<int64_t> lng;
   while (k < nblocks && p->sorted_len[k] >= 2048 && (double)p->sorted_len[k] * wlat > T) {
@@ -447,16 +457,18 @@ uint64_t* g_diag = nullptr;  // diagnostic build: per-segment cycle sums of the 
 #endif
 
 // tname: kernel timer (nullptr: none); max_grid > 0 caps the persistent grid
+// cus: the CUs the launch's stream may use (default: all)
 int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
-              int64_t max_grid = -1) {
+              int64_t max_grid = -1, int cus = 0) {
   itr::SweepGeometry g = itr::sweep_geometry(a.n, mode);
   if (g.iq < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", a.n);
   a.xp = g.xp;
-  int64_t grid = (int64_t)g.per_cu * cu_count();
+  if (cus <= 0) cus = cu_count();
+  int64_t grid = (int64_t)g.per_cu * cus;
   if (grid > a.nblocks) grid = a.nblocks;
   if (max_grid > 0 && grid > max_grid) grid = max_grid;
   if (grid <= 0) return 0;
-  if (grid <= cu_count()) g.lds = std::max(g.lds, itr::kExclusiveLds);  // one per CU
+  if (grid <= cus) g.lds = std::max(g.lds, itr::kExclusiveLds);  // one per CU
   HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
 #ifdef ITR_DIAG
   if (getenv("ITR_VERBOSE"))
@@ -483,7 +495,8 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
 // counters on `st` first (a split launch resets them once, before both parts).
 int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const itr::MfmaGeometry& g,
                hipStream_t st, const char* tname, bool valu = true, bool mfma = true,
-               int64_t max_grid = -1, bool zero_queues = true) {
+               int64_t max_grid = -1, bool zero_queues = true, int cus = 0) {
+  if (cus <= 0) cus = cu_count();
   itr::MfmaArgs a{};
   a.n = m->n;
   const bool ll = mode == itr::MODE_FWD_LL;
@@ -529,11 +542,11 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_HYB_PER_CU")) per_cu = atoi(getenv("ITR_HYB_PER_CU"));
 #endif
-  int64_t grid = std::min<int64_t>((int64_t)per_cu * cu_count(), work);
+  int64_t grid = std::min<int64_t>((int64_t)per_cu * cus, work);
   if (max_grid > 0) grid = std::min(grid, max_grid);
   if (grid <= 0) return 0;
   itr::MfmaGeometry gx = g;
-  if (grid <= cu_count()) gx.lds_min = itr::kExclusiveLds;  // one workgroup per CU
+  if (grid <= cus) gx.lds_min = itr::kExclusiveLds;  // one workgroup per CU
   if (zero_queues) HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
 #ifdef ITR_DIAG
   if (getenv("ITR_VERBOSE"))
@@ -546,6 +559,9 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   HIP_TRY(itr::launch_hybrid_sweep(mode, gx, (int)grid, a, v, st));
   return 0;
 }
+
+int forward_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* loglik,
+                 hipStream_t st, int cus);
 
 }  // namespace
 
@@ -994,7 +1010,16 @@ int itr_forward_loglik(itr_model_t m, itr_plan_t p, const uint16_t* obs, double*
   if (int e = check_plan(p)) return e;
   if (p->nblocks == 0) return 0;
   if ((!obs && p->total > 0) || !loglik) return fail(ITR_EINVAL, "null device pointer");
-  hipStream_t st = (hipStream_t)stream;
+  return forward_impl(m, p, obs, loglik, (hipStream_t)stream, 0);
+}
+
+}  // extern "C"
+
+namespace {
+
+// the forward log-likelihood sweep on a stream that may use `cus` CUs (0: all)
+int forward_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* loglik,
+                 hipStream_t st, int cus) {
   itr::SweepArgs a = base_args(m, p, obs);
   a.mat = m->a;
   a.matT = m->aT;
@@ -1044,20 +1069,18 @@ int itr_forward_loglik(itr_model_t m, itr_plan_t p, const uint16_t* obs, double*
   if (g.cfg >= 0 && p->ngroups_ll > 0) {
     a.tasks = p->d_utasks;
     a.nblocks = p->nutasks;
-    if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, st, "forward")) return e;
+    if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, st, "forward", true, true, -1, true,
+                           cus))
+      return e;
     HIP_TRY(itr::launch_fwd_split_combine(m->n, g.xr, (int)p->nhsplit, p->d_hsplit_blk,
                                           p->d_svec, p->d_sK, loglik, st));
     return 0;
   }
-  if (int e = run_sweep(itr::MODE_FWD_LL, a, st, "forward")) return e;
+  if (int e = run_sweep(itr::MODE_FWD_LL, a, st, "forward", -1, cus)) return e;
   HIP_TRY(itr::launch_fwd_split_combine(m->n, xr, (int)p->nsplit, p->d_split_blk, p->d_svec,
                                         p->d_sK, loglik, st));
   return 0;
 }
-
-}  // extern "C"
-
-namespace {
 
 // The Viterbi sweep and traceback of every block into `path`; with fwd_loglik, the forward
 // log-likelihood sweep too, overlapped with the Viterbi sweep's longest blocks.
@@ -1099,22 +1122,25 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   // of the chip), instead of one after the other
   const bool few = !wave && fwd_loglik && p->nblocks <= cus - cus / 4;
   if (few) {
-    // unmasked streams: with one CU per Viterbi block masked off, the forward's halves
-    // queue for the remaining CUs; unmasked, the dispatcher places a forward workgroup beside
-    // a Viterbi block (100 x 100 kbp: 62 -> 36.5 ms, profiles/r3t_partition.txt)
+    // the Viterbi blocks alone on their CUs (masked), the forward on the others with as
+    // many workgroups per CU as it needs to run every task at once (100 x 100 kbp: 200
+    // halves on 156 CUs; one per CU queued a second round: 62 ms, unmasked 36.5 ms,
+    // profiles/r3t_partition.txt)
     Partition* pt = nullptr;
-    if (int e = partition((int)p->nblocks, 0, &pt, false)) return e;
+    const int X = (cus % 8 == 0) ? 8 : 1;
+    const int rv = (int)std::min<int64_t>((p->nblocks + X - 1) / X * X, cus - cus / 4);
+    if (int e = partition(rv, 0, &pt)) return e;
     HIP_TRY(hipEventRecord(pt->fork, st));
     HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
     HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
-    if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, p->nblocks)) return e;
-    if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, pt->blk)) return e;
+    if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, p->nblocks, rv)) return e;
+    if (int e = forward_impl(m, p, obs, fwd_loglik, pt->blk, cus - rv)) return e;
     HIP_TRY(hipEventRecord(pt->jl, pt->lng));
     HIP_TRY(hipEventRecord(pt->jb, pt->blk));
     HIP_TRY(hipStreamWaitEvent(st, pt->jl, 0));
     HIP_TRY(hipStreamWaitEvent(st, pt->jb, 0));
   } else if (!wave && fwd_loglik) {  // no overlap: the forward sweep first, on st
-    if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, st)) return e;
+    if (int e = forward_impl(m, p, obs, fwd_loglik, st, 0)) return e;
   }
   if (wave) {
     itr::VitArgs w{};
@@ -1158,12 +1184,18 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     af.nblocks = p->nutasks;
     af.svec = p->d_svec;
     af.sK = p->d_sK;
-    const int64_t rf = split_fwd ? p->fwd_reserve : 0;
+    // (the forward's reserved set exists without the forward too — one partition, one set
+    // of streams per plan — and then runs bulk blocks from the start)
+    const int64_t rf = p->fwd_reserve;
     const int64_t rv = nlong > 0 ? std::max(1, p->vit_reserve) : 0;
     // whole XCC sets: a mask that leaves an XCC without a reserved CU does not mask it at all
     const int X = (cus % 8 == 0) ? 8 : 1;
-    const int rvr = (int)std::min<int64_t>((rv + X - 1) / X * X, cus / 2);
-    const int rfr = (int)std::min<int64_t>((rf + X - 1) / X * X, cus / 4);
+    int Xr = X;  // rounding unit of the reserved sets
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_SE_ROUND")) Xr = 4 * X;  // one CU per shader engine
+#endif
+    const int rvr = (int)std::min<int64_t>((rv + Xr - 1) / Xr * Xr, cus / 2);
+    const int rfr = (int)std::min<int64_t>((rf + Xr - 1) / Xr * Xr, cus / 4);
     const int reserve_cus = rvr + rfr;
     if (split_fwd) {
       HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
@@ -1183,8 +1215,8 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
         a.nblocks = nlong;
         if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, rvr)) return e;
       }
+      HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
       if (split_fwd) {
-        HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
         if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, pt->lng2, nullptr, true, false,
                                rfr, false))
           return e;
@@ -1233,7 +1265,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
                                (int64_t)gf.per_cu * ocus, false))
           return e;
       } else if (fwd_loglik) {
-        if (int e = itr_forward_loglik(m, p, obs, fwd_loglik, sb)) return e;
+        if (int e = forward_impl(m, p, obs, fwd_loglik, sb, ocus)) return e;
       }
       if (w.nblocks > 0) {  // the per-wave sweep: after the forward's matrix-core groups
         const int64_t grid = std::min<int64_t>((int64_t)wv.per_cu * ocus, (w.nblocks + 3) / 4);
@@ -1249,10 +1281,8 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       HIP_TRY(hipEventRecord(pt->jb, pt->blk));
       HIP_TRY(hipStreamWaitEvent(st, pt->jl, 0));
       HIP_TRY(hipStreamWaitEvent(st, pt->jb, 0));
-      if (split_fwd) {
-        HIP_TRY(hipEventRecord(pt->jl2, pt->lng2));
-        HIP_TRY(hipStreamWaitEvent(st, pt->jl2, 0));
-      }
+      HIP_TRY(hipEventRecord(pt->jl2, pt->lng2));
+      HIP_TRY(hipStreamWaitEvent(st, pt->jl2, 0));
     }
     if (split_fwd)  // log P of the split blocks from their two halves
       HIP_TRY(itr::launch_fwd_split_combine(m->n, gf.xr, (int)p->nhsplit, p->d_hsplit_blk,

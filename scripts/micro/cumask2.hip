@@ -58,6 +58,13 @@ int main() {
   v.clear();
   for (int i = 0; i < cus; ++i) if ((i / 8) % 4 != 0) v.push_back(i);
   add("not_oct", v);
+  for (int k = 0; k < cus / 8; ++k) {  // local CU index k in every XCC
+    v.clear();
+    for (int x = 0; x < 8; ++x) v.push_back(8 * k + x);
+    char nm[16];
+    snprintf(nm, sizeof nm, "local%d", k);
+    add(nm, v);
+  }
   for (auto& M : masks) {
     std::vector<uint32_t> m((cus + 31) / 32, 0);
     for (int b : M.second) m[b / 32] |= 1u << (b % 32);

@@ -198,3 +198,39 @@ def test_vanloan_paths_compact_supports(gpu, n, ncls):
     spm = np.array([w for i in sel for w in paths[i][1]], dtype=np.int32)
     sub = vanloan_paths(Q, t, masks, job[sel], soff, spm, job_norm=norms).cpu().numpy()
     assert np.array_equal(sub, got[sel])
+
+
+def test_vanloan_paths_interval_branch_vs_per_path(gpu):
+    """One Pade branch and scaling per interval (itr_vanloan_paths: chosen from the largest
+    ||C_p t||_1 of the interval's paths) against the reference's per-path choice
+    (expm.py:9-167, here the device's per-matrix branch selection in expm_blocktri_batched):
+    paths of length 1 and 5 with empty and full masks in ONE interval, whose norms straddle
+    the Pade-9 / Pade-13 threshold (theta_9 = 2.10), so the short paths get a higher degree
+    and more squarings than the reference would give them.  The results agree to rounding
+    (1e-13 of the block's scale), which is the deviation DESIGN.md §4 states."""
+    from itrails_amd.dense import expm_blocktri_batched, vanloan_paths
+    rng = np.random.default_rng(4242)
+    n = 40
+    Q = rng.random((n, n)) * (rng.random((n, n)) < 0.3)
+    np.fill_diagonal(Q, 0.0)
+    np.fill_diagonal(Q, -Q.sum(axis=1))
+    Q /= np.abs(Q).sum(axis=0).max()  # ||Q||_1 = 1
+    masks = np.stack([np.zeros(n), np.ones(n), (rng.random(n) < 0.5)]).astype(np.uint8)
+    t = np.array([1.2])  # ||Q t|| = 1.2 < theta_9; five full-mask blocks: ~3 > theta_9
+    paths = [[0], [1], [0, 0, 0, 0, 0], [1, 1, 1, 1, 1], [2, 1, 2], [0, 2, 1, 1, 0]]
+    job = np.zeros(len(paths), dtype=np.int32)
+    off = np.zeros(len(paths) + 1, dtype=np.int64)
+    np.cumsum([len(p) for p in paths], out=off[1:])
+    pm = np.array([w for p in paths for w in p], dtype=np.int32)
+    got = vanloan_paths(Q, t, masks, job, off, pm).cpu().numpy()
+    for k, p in enumerate(paths):
+        L = len(p)
+        C = np.zeros((n * L, n * L))
+        for b in range(L):
+            C[b * n:(b + 1) * n, b * n:(b + 1) * n] = Q
+        for b in range(1, L):
+            C[(b - 1) * n:b * n, b * n:(b + 1) * n] = masks[p[b - 1]][:, None] * Q * \
+                masks[p[b]][None, :]
+        ref = expm_blocktri_batched((C * t[0])[None], L)[0][:n, -n:]
+        scale = max(np.abs(ref).max(), 1.0)
+        assert np.abs(got[k] - ref).max() <= 1e-13 * scale, (k, np.abs(got[k] - ref).max())
