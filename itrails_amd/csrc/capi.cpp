@@ -1127,7 +1127,9 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     // halves on 156 CUs; one per CU queued a second round: 62 ms, unmasked 36.5 ms,
     // profiles/r3t_partition.txt)
     Partition* pt = nullptr;
-    const int X = (cus % 8 == 0) ? 8 : 1;
+    // one CU per block in whole shader-engine sets (32 CUs: one per engine of every XCC):
+    // the dispatcher deals the blocks' workgroups to the engines in turn
+    const int X = (cus % 32 == 0) ? 32 : 1;
     const int rv = (int)std::min<int64_t>((p->nblocks + X - 1) / X * X, cus - cus / 4);
     if (int e = partition(rv, 0, &pt)) return e;
     HIP_TRY(hipEventRecord(pt->fork, st));

@@ -86,6 +86,45 @@ struct MLds {
   static constexpr size_t bytes = kf_off + (size_t)GB * 4 * 4;
 };
 
+// y[gb] = x_gb(row ra, sources kk NK ..) @ B for the GB groups of a task: the A operands
+// (four per group) are read one k-step ahead and the groups' MFMAs interleaved, so an LDS
+// round trip hides under 4 GB MFMAs.  The empty asm keeps the compiler from hoisting every
+// read to the top (their registers would spill the matrix slice) or from serialising them
+// into one register quad (a full LDS round trip per two MFMAs: the round-2 code at N = 133)
+template <int NK, int GB>
+__device__ __forceinline__ void mfma_chain(const double* const (&xs)[GB], const double (&B)[NK],
+                                           double (&y)[GB]) {
+  constexpr int W = 2;  // A operands per group per k-step (one ds_read_b128)
+  double acc[GB][2], cur[GB][W], nxt[GB][W];
+#pragma unroll
+  for (int gb = 0; gb < GB; ++gb) {
+    acc[gb][0] = acc[gb][1] = 0.0;
+#pragma unroll
+    for (int u = 0; u < W; ++u) cur[gb][u] = u < NK ? xs[gb][u] : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < NK; q += W) {
+    if (q + W < NK) {
+#pragma unroll
+      for (int gb = 0; gb < GB; ++gb)
+#pragma unroll
+        for (int u = 0; u < W; ++u) nxt[gb][u] = q + W + u < NK ? xs[gb][q + W + u] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < W; ++u)
+#pragma unroll
+      for (int gb = 0; gb < GB; ++gb)
+        if (q + u < NK) acc[gb][u & 1] = mfma4(cur[gb][u], B[q + u], acc[gb][u & 1]);
+#pragma unroll
+    for (int gb = 0; gb < GB; ++gb)
+#pragma unroll
+      for (int u = 0; u < W; ++u) cur[gb][u] = nxt[gb][u];
+    asm volatile("" ::: "memory");
+  }
+#pragma unroll
+  for (int gb = 0; gb < GB; ++gb) y[gb] = acc[gb][0] + acc[gb][1];
+}
+
 // One task of the matrix-core sweep: the GB groups g0 .. g0+GB-1 of p.groups.
 template <int NT, int NK, int GB, int MODE>
 __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem, int g0) {
@@ -228,19 +267,10 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
             if (t >= 1 && t < Tmax) {
               const int buf = (t - 1) & 1;
               double y[GB];
+              const double* xs[GB];
 #pragma unroll
-              for (int gb = 0; gb < GB; ++gb) {
-                const double* xs = &X[gb][buf][ra][kk * NK];
-                double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-#pragma unroll
-                for (int s = 0; s < NK; s += 4) {
-                  a0 = mfma4(xs[s], B[s], a0);
-                  if (s + 1 < NK) a1 = mfma4(xs[s + 1], B[s + 1], a1);
-                  if (s + 2 < NK) a2 = mfma4(xs[s + 2], B[s + 2], a2);
-                  if (s + 3 < NK) a3 = mfma4(xs[s + 3], B[s + 3], a3);
-                }
-                y[gb] = (a0 + a1) + (a2 + a3);
-              }
+              for (int gb = 0; gb < GB; ++gb) xs[gb] = &X[gb][buf][ra][kk * NK];
+              mfma_chain<NK, GB>(xs, B, y);
 #pragma unroll
               for (int gb = 0; gb < GB; ++gb) {
                 double sc = 1.0;
@@ -361,19 +391,15 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
                 if (jv) X[gb][buf][r][j] = v;
               }
               lds_barrier();
+              // the matrix products first; the columns' normalisation (a log-depth tree over
+              // the NT wave partials) and the rescale maximum while they run
+              double y[GB];
+              const double* xs[GB];
+#pragma unroll
+              for (int gb = 0; gb < GB; ++gb) xs[gb] = &X[gb][buf][ra][kk * NK];
+              mfma_chain<NK, GB>(xs, B, y);
 #pragma unroll
               for (int gb = 0; gb < GB; ++gb) {
-                // the matrix product first; the column's normalisation (a log-depth tree over
-                // the NT wave partials) and the rescale maximum while it runs
-                const double* xs = &X[gb][buf][ra][kk * NK];
-                double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-#pragma unroll
-                for (int q = 0; q < NK; q += 4) {
-                  a0 = mfma4(xs[q], B[q], a0);
-                  if (q + 1 < NK) a1 = mfma4(xs[q + 1], B[q + 1], a1);
-                  if (q + 2 < NK) a2 = mfma4(xs[q + 2], B[q + 2], a2);
-                  if (q + 3 < NK) a3 = mfma4(xs[q + 3], B[q + 3], a3);
-                }
                 const double rS = recip_nr(tree_sum<NT>(&RS[gb][buf][r][0]));
                 if (s < T[gb] && jv) p.post[(c0[gb] + (T[gb] - 1 - s)) * n + j] = qv[gb] * rS;
                 double sc = 1.0;
@@ -383,7 +409,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
                   for (int v = 1; v < NT; ++v) M = fmax(M, RM[gb][v][r]);
                   if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
                 }
-                bt[gb] = ((a0 + a1) + (a2 + a3)) * sc;
+                bt[gb] = y[gb] * sc;
               }
             }
           }
