@@ -194,8 +194,9 @@ def pmc_rates(n):
     """Issue and matrix-core counters of the sweep kernels from the latest committed
     rocprofv3 --pmc summary (scripts/gpu_r3g.sh -> scripts/pmc_summary.py): per kernel the
     share of SIMD-cycles with the MFMA pipe busy (SQ_VALU_MFMA_BUSY_CYCLES) and with FP64 VALU
-    work issued (SQ_INSTS_VALU x 4 cycles), normalised to the SIMDs of the CUs the launch ran
-    on, plus the waves' waitcnt share (SQ_WAIT_ANY / SQ_WAVE_CYCLES)."""
+    work issued (SQ_INSTS_VALU x 4 cycles), as shares of all SIMDs of the chip over the
+    launch's duration (a launch on a CU subset scores its share of the whole chip), plus the
+    waves' waitcnt share (SQ_WAIT_ANY / SQ_WAVE_CYCLES)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))
     for f in reversed(files):
         d = json.load(open(f))
@@ -204,13 +205,7 @@ def pmc_rates(n):
             if v.get("n_states", 70) != n or "mfma_util" not in v or \
                     not ("sweep_kernel" in name or "wave_" in name):
                 continue
-            # CU share of the launch: the combined call's bulk kernels run on 192 of 256 CUs
-            # (the others are reserved for the long blocks), the long-block sweep on 40
-            share = 1.0
-            if "wave_mixed_kernel" in name or "wave_vit_kernel" in name:
-                share = 192 / 256
-            elif name.startswith("void itr::sweep_kernel<") and name.endswith(", 3>(itr::SweepArgs)"):
-                share = 40 / 256
+            share = 1.0  # shares of all SIMDs of the chip (launches run on CU subsets)
             short = re.sub(r"\(itr::.*$", "", name.replace("void itr::", "")
                            .replace("(anonymous namespace)::", ""))
             out[short] = {"mfma_busy": round(v["mfma_util"] / share, 3),
