@@ -262,7 +262,8 @@ struct itr_plan {
   int32_t* d_order = nullptr;
   int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep,
                            // [3, 4] hybrid sweeps, [5, 6] Viterbi hybrid, [7] per-wave Viterbi,
-                           // [8, 9] the idle loop of a split hybrid launch, [10] per-wave forward
+                           // [8, 9] the idle loop of a split hybrid launch, [10] per-wave forward,
+                           // [12] mixed launch, [13] the long blocks' traceback
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
   std::vector<int64_t> sorted_len;  // block lengths, longest first (processing order)
@@ -1112,6 +1113,26 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   a.alpha = p->d_alpha;
   a.stay = p->d_stay;
   a.last_state = p->d_last;
+  // traceback of blocks order[from, from + count) (vit_trace_kernel); the long blocks'
+  // tracebacks run on their reserved CUs right after their Viterbi sweep (`traced` of them),
+  // the rest after the join
+  auto trace_args = [&]() {
+    itr::TraceArgs ta{};
+    ta.n = m->n;
+    ta.xr = vit_stride(m->n);
+    ta.off = p->d_off;
+    ta.tile_off = p->d_tile_off;
+    ta.queue = p->d_queue + 1;
+    ta.obs = obs;
+    ta.log_a = m->la;
+    ta.log_e = m->LE;
+    ta.ckpt = p->d_alpha;
+    ta.stay = p->d_stay;
+    ta.last_state = p->d_last;
+    ta.path = path;
+    return ta;
+  };
+  int64_t traced = 0;
   const itr::WaveVitGeometry wv = itr::wave_vit_geometry(m->n);
   bool wave = wv.iq > 0 && m->LEW && m->xrw == wv.xr;
   const int cus = cu_count();
@@ -1205,6 +1226,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     }
     // before the fork: the bulk queue is shared with the reserved CUs' late launch
     HIP_TRY(hipMemsetAsync(mixed ? p->d_queue + 12 : w.queue, 0, sizeof(int), st));
+    if (nlong > 0) HIP_TRY(hipMemsetAsync(p->d_queue + 13, 0, sizeof(int), st));
     if (reserve_cus > 0) {
       // the long blocks' Viterbi on lng (rvr CUs), the forward's VALU halves on lng2 (rfr
       // others): separate masks, so each set joins the bulk queue as soon as its own long
@@ -1216,6 +1238,13 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       if (nlong > 0) {
         a.nblocks = nlong;
         if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, rvr)) return e;
+        itr::TraceArgs tl = trace_args();
+        tl.nblocks = nlong;
+        tl.order = p->d_order;
+        tl.queue = p->d_queue + 13;
+        HIP_TRY(itr::launch_vit_traceback(tl, (int)std::min<int64_t>((nlong + 3) / 4, 4 * rvr),
+                                          pt->lng));
+        traced = nlong;
       }
       HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
       if (split_fwd) {
@@ -1293,26 +1322,14 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
   }
   both.reset();
-  itr::TraceArgs ta{};
-  ta.n = m->n;
-  ta.xr = vit_stride(m->n);
-  ta.nblocks = p->nblocks;
-  ta.off = p->d_off;
-  ta.tile_off = p->d_tile_off;
-  ta.order = p->d_order;
-  ta.queue = p->d_queue + 1;
-  ta.obs = obs;
-  ta.log_a = m->la;
-  ta.log_e = m->LE;
-  ta.ckpt = p->d_alpha;
-  ta.stay = p->d_stay;
-  ta.last_state = p->d_last;
-  ta.path = path;
+  itr::TraceArgs ta = trace_args();
+  ta.nblocks = p->nblocks - traced;
+  ta.order = p->d_order + traced;
   // one wave per block, 4 waves per workgroup (LDS: 4 x 16 recomputed rows)
-  const int64_t grid = std::min<int64_t>((p->nblocks + 3) / 4, (int64_t)cu_count() * 4);
+  const int64_t grid = std::min<int64_t>((ta.nblocks + 3) / 4, (int64_t)cu_count() * 4);
   HIP_TRY(hipMemsetAsync(ta.queue, 0, sizeof(int), st));
   Scope sc("traceback", st);
-  HIP_TRY(itr::launch_vit_traceback(ta, (int)grid, st));
+  if (ta.nblocks > 0) HIP_TRY(itr::launch_vit_traceback(ta, (int)grid, st));
   return 0;
 }
 
