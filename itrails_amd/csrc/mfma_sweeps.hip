@@ -95,10 +95,12 @@ template <int NK, int GB>
 __device__ __forceinline__ void mfma_chain(const double* const (&xs)[GB], const double (&B)[NK],
                                            double (&y)[GB]) {
   constexpr int W = 2;  // A operands per group per k-step (one ds_read_b128)
-  double acc[GB][2], cur[GB][W], nxt[GB][W];
+  // four accumulator chains per group (source s into chain s % 4: the 52-cycle dependent
+  // MFMA latency under 4 x 16 issue cycles), summed as (0 + 1) + (2 + 3)
+  double acc[GB][4], cur[GB][W], nxt[GB][W];
 #pragma unroll
   for (int gb = 0; gb < GB; ++gb) {
-    acc[gb][0] = acc[gb][1] = 0.0;
+    acc[gb][0] = acc[gb][1] = acc[gb][2] = acc[gb][3] = 0.0;
 #pragma unroll
     for (int u = 0; u < W; ++u) cur[gb][u] = u < NK ? xs[gb][u] : 0.0;
   }
@@ -114,7 +116,7 @@ __device__ __forceinline__ void mfma_chain(const double* const (&xs)[GB], const 
     for (int u = 0; u < W; ++u)
 #pragma unroll
       for (int gb = 0; gb < GB; ++gb)
-        if (q + u < NK) acc[gb][u & 1] = mfma4(cur[gb][u], B[q + u], acc[gb][u & 1]);
+        if (q + u < NK) acc[gb][(q + u) & 3] = mfma4(cur[gb][u], B[q + u], acc[gb][(q + u) & 3]);
 #pragma unroll
     for (int gb = 0; gb < GB; ++gb)
 #pragma unroll
@@ -122,7 +124,7 @@ __device__ __forceinline__ void mfma_chain(const double* const (&xs)[GB], const 
     asm volatile("" ::: "memory");
   }
 #pragma unroll
-  for (int gb = 0; gb < GB; ++gb) y[gb] = acc[gb][0] + acc[gb][1];
+  for (int gb = 0; gb < GB; ++gb) y[gb] = (acc[gb][0] + acc[gb][1]) + (acc[gb][2] + acc[gb][3]);
 }
 
 // One task of the matrix-core sweep: the GB groups g0 .. g0+GB-1 of p.groups.
