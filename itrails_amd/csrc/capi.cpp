@@ -781,10 +781,12 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
     return sorted;
   };
   std::vector<int32_t> tasks = make_tasks(nblocks);
-  // groups of four `tasks` ids for the per-wave matrix-core forward: forward-shaped tasks and
-  // backward halves apart (a group shares its matrix operand), each kind longest first (the
-  // task list is sorted longest first)
+  // groups of four `tasks` ids for the per-wave matrix-core forward on its own
+  // (ITR_WAVE_FWD, experiment library only): forward-shaped tasks and backward halves apart (a
+  // group shares its matrix operand), each kind longest first (the task list is sorted
+  // longest first)
   std::vector<int32_t> wgroups;
+#ifdef ITR_EXPERIMENT
   {
     std::vector<int32_t> fw, bw;
     for (int64_t k = 0; k < (int64_t)tasks.size() / 3; ++k)
@@ -802,6 +804,7 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
       for (int r = 0; r < 4; ++r) wgroups.push_back(i < v.size() ? v[i++] : -1);
     }
   }
+#endif
   // Hybrid sweeps (mfma_sweeps.hip).  A matrix-core group steps four blocks in about twice
   // the VALU step time, so the longest work stays on the lower-latency VALU path and the
   // bulk goes through the matrix cores.  Forward log-likelihood, with
