@@ -176,9 +176,15 @@ def pmc_traffic(n, mode, tag_hint=""):
                                                (k.startswith("void itr::sweep_kernel<") and
                                                 k.endswith(", 3>(itr::SweepArgs)")))]
             if len(parts) == 2:
-                return round(sum(v["hbm_bytes_raw"] for _, v in parts)), (
+                # the per-wave kernel runs as the bulk launch plus one launch per reserved set
+                # that joins the queue: its per-dispatch average times its launches per call
+                # (the profiled command, scripts/gpu_r3final.sh, makes 3 itr_viterbi calls)
+                def per_call(k, v):
+                    return v["hbm_bytes_raw"] * (max(1, round(v.get("calls", 3) / 3))
+                                                 if "wave_vit_kernel" in k else 1)
+                return round(sum(per_call(k, v) for k, v in parts)), (
                     f"{os.path.basename(f)} (" + " + ".join(k for k, _ in parts) +
-                    "): FETCH_SIZE+WRITE_SIZE per call, raw")
+                    "): FETCH_SIZE+WRITE_SIZE per call (all launches of each kernel), raw")
         for name, v in d.items():
             hyb = re.search(r"hybrid_sweep_kernel<\d+, \d+, \d+, (\d+),", name)
             if ((name.startswith("void itr::sweep_kernel<") and
