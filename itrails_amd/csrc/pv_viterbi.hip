@@ -116,8 +116,9 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
   double* S = wl;                                          // [PV_K + 1][rss] value rows
   double* EC = S + (PV_K + 1) * rss;                       // [PV_K][rs] the half-tile's log e
   double* MG = EC + PV_K * rs;                             // [rs] scanned margins
-  uint32_t* FB = reinterpret_cast<uint32_t*>(MG + rs);     // [rs] scanned flags | mis << 16
-  int* WIN = reinterpret_cast<int*>(FB + rs);              // [rs] new maximising sources
+  double* SINK = MG + rs;                                  // [64] stores of lanes without a slot
+  uint32_t* FB = reinterpret_cast<uint32_t*>(SINK + 64);   // [rs + 64] flags | mis << 16
+  int* WIN = reinterpret_cast<int*>(FB + rs + 64);         // [rs] new maximising sources
   uint16_t* LIST = reinterpret_cast<uint16_t*>(WIN + rs);  // [lcap] pairs (k << 8 | j)
   uint16_t* SYM = LIST + a.lcap;                           // [2][64] observed symbols
 
@@ -137,15 +138,20 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
   wave_lds_sync();
   auto sym = [&](int c) -> int { return SYM[((c >> 6) & 1) * 64 + (c & 63)]; };
 
-  int jt[NS], je[NS];
-  bool act[NS], inr[NS];
+  // slot s of lane l: target jt = 64 s + l; a lane whose target is outside the LDS rows
+  // stores into SINK and reads a clamped column (its values are -inf and never counted)
+  int jt[NS], jc[NS], je[NS];
+  bool act[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     jt[s] = 64 * s + l;
     act[s] = jt[s] < n;
-    inr[s] = jt[s] < rs;            // has a slot in the LDS rows
-    je[s] = min(jt[s], xe - 1);     // clamped log-emission column
+    jc[s] = min(jt[s], rs - 1);
+    je[s] = min(jt[s], xe - 1);
   }
+  auto row_st = [&](int row, int s) -> double* {  // this lane's slot in a value row (or SINK)
+    return jt[s] < rs ? S + row * rss + jt[s] : SINK + l;
+  };
   // log e rows of half-tile h into registers (global loads, waited for a half-tile later)
   double en[PV_K][NS];
   auto e_issue = [&](int h) {
@@ -185,7 +191,7 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
   bool stayp[NS];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    p[s] = act[s] ? jt[s] : 0;
+    p[s] = jc[s];
     lap[s] = ld[s];
     stayp[s] = act[s];
     L[s] = -INFINITY;
@@ -208,15 +214,14 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
 #pragma unroll
     for (int k = 0; k < PV_K; ++k)
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
-        if (inr[s]) EC[k * rs + jt[s]] = act[s] ? en[k][s] : -INFINITY;
-    // this lane's log e_j of window column k (the padding lanes' -inf included)
-    auto ecol = [&](int k, int s) -> double { return inr[s] ? EC[k * rs + jt[s]] : -INFINITY; };
+      for (int s = 0; s < NS; ++s) *(jt[s] < rs ? EC + k * rs + jt[s] : SINK + l) = act[s] ? en[k][s] : -INFINITY;
     if ((cb & 63) == 0 && cb > 0) {  // next symbol chunk in, the one after requested
       SYM[(((cb >> 6) + 1) & 1) * 64 + l] = clamp_sym(sin);
       sin = symg(cb + 128 + l);
     }
     wave_lds_sync();
+    // this lane's log e of a half-tile column (padding lanes: -inf)
+    auto ecol = [&](int k, int s) -> double { return act[s] ? EC[k * rs + jc[s]] : -INFINITY; };
     if (cb + PV_K < T) e_issue(h + 1);
     int kstart = h == 0 ? 1 : 0;
     const int kend = min(PV_K, T - cb);
@@ -227,10 +232,8 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
       // ---- 1. prediction of columns cb + kstart .. cb + kend - 1 -----------------------
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        if (inr[s]) {
-          S[kstart * rss + jt[s]] = x[s];  // the committed column: row kstart
-          FB[jt[s]] = 0u;
-        }
+        *row_st(kstart, s) = x[s];  // the committed column: row kstart
+        FB[jt[s] < rs ? jt[s] : rs + l] = 0u;
       }
 #pragma unroll
       for (int k = 0; k < PV_K; ++k)
@@ -254,7 +257,7 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
           for (int s = 0; s < NS; ++s) {
             const double v = (src[s] + lap[s]) + ecol(k, s);
             sv[k + 1][s] = v;
-            if (inr[s]) S[(k + 1) * rss + jt[s]] = v;
+            *row_st(k + 1, s) = v;
           }
         }
       }
@@ -287,16 +290,16 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
         om = fmax(om, dpp_f64<DPP_HM>(om));
         dmx = fmax(dmx, dpp_f64<DPP_HM>(dmx));
       }
+      // the predicted source's change from row k to k + 1 (stays: the target's own)
+      auto dps = [&](int k, int s) -> double {
+        if (anysw) return pv_delta(S[(k + 1) * rss + p[s]], S[k * rss + p[s]]);
+        return pv_delta(sv[k + 1][s], sv[k][s]);
+      };
       // tests: a pair passes by its carried margin bound or by the plain bound of a stay
       // (yd > max_i omega_i + max_{i != j} log a_ij + log e_j); a target failing once is
       // scanned for the rest of the window
       uint32_t fb[NS];  // this lane's failing window columns (bit k)
-      double L0[NS];
-      // the predicted source's change from row k to k + 1
-      auto dpk = [&](int k, int s) -> double {
-        if (anysw) return pv_delta(S[(k + 1) * rss + p[s]], S[k * rss + p[s]]);
-        return pv_delta(sv[k + 1][s], sv[k][s]);
-      };
+      double L0[NS];    // the bound at the window's first column
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         fb[s] = 0;
@@ -310,17 +313,17 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
           const double thr = 1e-6 + fabs(o1) * 0x1p-40;
 #pragma unroll
           for (int s = 0; s < NS; ++s) {
-            const double dp = dpk(k, s);
             const double bnd = (o1 + mj[s]) + ecol(k, s);
-            const bool pass = fb[s] == 0 && (L[s] > thr || (stayp[s] && sv[k + 1][s] > bnd));
-            const bool fail = act[s] && !pass;
-            fb[s] |= (uint32_t)fail << k;
-            L[s] = pv_adv(L[s], dp, dm);
+            const bool c1 = L[s] > thr;
+            const bool c2 = sv[k + 1][s] > bnd;
+            const bool pass = (fb[s] == 0u) & (c1 | (stayp[s] & c2));
+            fb[s] |= (uint32_t)(act[s] & !pass) << k;
+            L[s] = pv_adv(L[s], dps(k, s), dm);
           }
         }
       }
       // pairs in (column, slot, lane) order; the list holds at most lcap pairs: the window
-      // ends before the column that would overflow it (one column has at most 64 NS = lcap)
+      // ends before the column that would overflow it (one column has at most 64 NS <= lcap)
       int kcut = kend, npairs = 0;
 #pragma unroll
       for (int k = 0; k < PV_K; ++k) {
@@ -347,11 +350,12 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
       PV_T(9);
       PV_CNT(3, npairs);
       // exact scans, one lane per pair, pairs in column order: the two largest candidates
-      // over the sources i != j, the stay, omega = max(yd, yo), the flag, the margin
+      // over the sources i != j, the stay, omega = max(yd, yo), the flag, the margin; the
+      // lane keeps the pairs of the window's last column and of the first mispredicted one
       int kmis = PV_K;  // first mispredicted window column (PV_K: none)
-      double exr[NS], mgr[NS];
-      int kr[NS], jr[NS];
-      bool mr[NS];
+      double exr[NS], mgr[NS];  // per round: this lane's pair's omega and margin
+      int kr[NS], jr[NS];       //   its column (-1: none) and target
+      bool mr[NS];              //   mispredicted
 #pragma unroll
       for (int rd = 0; rd < NS; ++rd) {
         kr[rd] = -1;
@@ -384,9 +388,9 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
           const double yo = z1 + ee;
           const double ex = fmax(yd, yo);
           const bool flg = yd > yo;
-          const bool mis = valid && ex != sr[rss + jj];
-          if (valid && (flg || mis))
-            atomicOr(&FB[jj], (flg ? 1u << k : 0u) | (mis ? 1u << (16 + k) : 0u));
+          const bool mis = valid & (ex != sr[rss + jj]);
+          const uint32_t bits = (flg ? 1u << k : 0u) | (mis ? 1u << (16 + k) : 0u);
+          if (valid & (bits != 0u)) atomicOr(&FB[jj], bits);
           const uint64_t mb = __ballot(mis);
           if (mb && kmis == PV_K) kmis = __builtin_amdgcn_readlane(k, __builtin_ctzll(mb));
           exr[rd] = ex;
@@ -400,16 +404,18 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
       // ---- 3. commit up to the first mispredicted column ----------------------------------
       const int kfin = kmis < PV_K ? kmis + 1 : kcut;  // window columns [kstart, kfin)
       const int kl = kfin - 1;                         // the last committed window column
-      double dml = lane_f64(dmx, 8 * kl);              // max change from row kl to kl + 1
+      // the pairs of column kl: margins (and, mispredicted, corrected values and the largest
+      // change of a corrected entry from row kl to kl + 1)
+      double dml = lane_f64(dmx, 8 * kl);
       {
         double dcor = -INFINITY;
 #pragma unroll
         for (int rd = 0; rd < NS; ++rd) {
           if (kr[rd] == kl) {
             MG[jr[rd]] = mgr[rd];
-            if (mr[rd]) {  // corrected value: row kl + 1 and its change from row kl
-              S[(kl + 1) * rss + jr[rd]] = exr[rd];
+            if (mr[rd]) {
               dcor = fmax(dcor, pv_delta(exr[rd], S[kl * rss + jr[rd]]));
+              S[(kl + 1) * rss + jr[rd]] = exr[rd];
             }
           }
         }
@@ -425,24 +431,28 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
         // lanes holding such a pair)
 #pragma unroll
         for (int rd = 0; rd < NS; ++rd) {
-          const bool srch = kr[rd] == kmis && mr[rd];
-          if (__ballot(srch)) {
+          const bool misk = (kr[rd] == kl) & mr[rd];
+          if (__ballot(misk)) {
             const int jj = jr[rd];
-            const double* sr = S + kmis * rss;
+            const double exk = exr[rd];
+            const double* sr = S + kl * rss;
             const double* lr = LAT + jj * rsa;
-            const double ee = EC[kmis * rs + jj];
+            const double ee = EC[kl * rs + jj];
             const double yd = (sr[jj] + LDG[jj]) + ee;
-            int f = yd >= exr[rd] ? jj : 0x7fffffff;
-            if (__ballot(srch && f != jj)) {
+            const bool look = misk & !(yd >= exk);
+            int f = jj;
+            if (__ballot(look)) {
+              f = 0x7fffffff;
 #pragma unroll 4
               for (int i = 0; i < np; i += 2) {
                 const pv_d2 sv2 = *reinterpret_cast<const pv_d2*>(sr + i);
                 const pv_d2 lv2 = *reinterpret_cast<const pv_d2*>(lr + i);
-                if ((sv2.y + lv2.y) + ee == exr[rd]) f = min(f, i + 1);
-                if ((sv2.x + lv2.x) + ee == exr[rd]) f = min(f, i);
+                f = ((sv2.y + lv2.y) + ee == exk) ? min(f, i + 1) : f;
+                f = ((sv2.x + lv2.x) + ee == exk) ? min(f, i) : f;
               }
+              f = look ? f : jj;
             }
-            if (srch) WIN[jj] = f;
+            if (misk) WIN[jj] = f;
           }
         }
       }
@@ -451,27 +461,27 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
       uint32_t fbw[NS];
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        fbw[s] = inr[s] ? FB[jt[s]] : 0u;
+        fbw[s] = FB[jc[s]];
         const uint32_t fl = ((stayp[s] ? ~fb[s] : 0u) | fbw[s]) & wm;
-        flw[s] |= fl << (8 * (h & 1));
-        x[s] = inr[s] ? S[kfin * rss + jt[s]] : -INFINITY;
-        // the margin bound at the next column: from the scan of column kl if the target
-        // was scanned there, else carried over the committed columns (the last change with
-        // the corrected row maximum)
-        double Ls = L0[s], dpl = 0.0;
+        flw[s] |= act[s] ? fl << (8 * (h & 1)) : 0u;
+        x[s] = act[s] ? S[kfin * rss + jc[s]] : -INFINITY;
+        // the margin bound at the next column: from the scan of column kl if the target was
+        // scanned there, else carried over the committed columns; the last change with the
+        // corrected row maximum
+        double Lb = L0[s], dpl = 0.0;
 #pragma unroll
         for (int k = 0; k < PV_K; ++k) {
-          if (k >= kstart && k < kl) Ls = pv_adv(Ls, dpk(k, s), lane_f64(dmx, 8 * k));
-          if (k == kl) dpl = dpk(k, s);
+          if (k >= kstart && k < kl) Lb = pv_adv(Lb, dps(k, s), lane_f64(dmx, 8 * k));
+          if (k == kl) dpl = dps(k, s);  // (rows after the correction of a misprediction)
         }
-        if (fb[s] & wm) Ls = inr[s] ? MG[jt[s]] : -INFINITY;
-        L[s] = pv_adv(Ls, dpl, dml);
+        const double mgs = MG[jc[s]];
+        Lb = (fb[s] & wm) ? mgs : Lb;
+        L[s] = pv_adv(Lb, dpl, dml);
       }
       if ((h & 1) == 0 && h > 0 && kstart == 0) {  // column cb = tile (h / 2)'s first column
 #pragma unroll
         for (int s = 0; s < NS; ++s)
-          buf_store_f64(rck, vo[s] * 8, (uint32_t)((h >> 1) * xr) * 8,
-                        S[rss + (inr[s] ? jt[s] : 0)]);
+          buf_store_f64(rck, vo[s] * 8, (uint32_t)((h >> 1) * xr) * 8, S[rss + jc[s]]);
       }
       PV_T(11);
       PV_CNT(1, kfin - kstart);
@@ -480,14 +490,14 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
         bool sw = false;
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-          if ((fbw[s] >> (16 + kmis)) & 1u) {
-            const int w = WIN[jt[s]];
-            p[s] = w;
-            lap[s] = w == jt[s] ? ld[s] : LAT[jt[s] * rsa + w];
-            L[s] = -INFINITY;
-          }
-          stayp[s] = act[s] && p[s] == jt[s];
-          sw = sw || (act[s] && p[s] != jt[s]);
+          const bool m = act[s] & (((fbw[s] >> (16 + kmis)) & 1u) != 0u);
+          const int w = WIN[jc[s]];
+          p[s] = m ? w : p[s];
+          const double lw = LAT[jc[s] * rsa + min(w, n - 1)];
+          lap[s] = m ? (w == jt[s] ? ld[s] : lw) : lap[s];
+          L[s] = m ? -INFINITY : L[s];
+          stayp[s] = act[s] & (p[s] == jt[s]);
+          sw = sw | (act[s] & (p[s] != jt[s]));
         }
         anysw = __ballot(sw) != 0;
       }
@@ -506,11 +516,11 @@ __device__ __forceinline__ void pv_task(const PvArgs& a, double* wl, const doubl
   double bv = act[0] ? x[0] : -INFINITY;
   int bj = act[0] ? jt[0] : 0x7fffffff;
 #pragma unroll
-  for (int s = 1; s < NS; ++s)
-    if (act[s] && x[s] > bv) {
-      bv = x[s];
-      bj = jt[s];
-    }
+  for (int s = 1; s < NS; ++s) {
+    const bool b = act[s] & (x[s] > bv);
+    bv = b ? x[s] : bv;
+    bj = b ? jt[s] : bj;
+  }
   wave_first_max(bv, bj);
   if (l == 0) a.last_state[blk] = (uint8_t)bj;
   PV_FLUSH();
@@ -525,7 +535,7 @@ __device__ __forceinline__ int pv_next(int* queue, int base) {
 }
 
 template <int NS>
-__global__ void __launch_bounds__(512) pv_vit_kernel(PvArgs a) {
+__global__ void __launch_bounds__(NS == 1 ? 512 : 256) pv_vit_kernel(PvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* LAT = reinterpret_cast<double*>(smem);
   double* LDG = LAT + (size_t)a.n * a.rsa;
@@ -563,13 +573,13 @@ PvGeometry pv_geometry(int n) {
   const int rss = rs + 2;                 // its stride (= 2 mod 4)
   const int xe = (n + 1) & ~1;            // padded log-emission row
   const int eb = 0;
-  const int lcap = 64 * ns;
-  // per wave: value rows, the half-tile's log e, margins, FB + WIN (rs ints each), pair list,
-  // symbols
-  const int wl = ((PV_K + 1) * rss + PV_K * rs + rs + rs + lcap / 4 + 32 + 1) & ~1;
+  const int lcap = 64 * ns;  // pairs scanned per window at most (one round per slot)
+  // per wave: value rows, the half-tile's log e, margins, sink, FB (rs + 64 ints), WIN (rs
+  // ints), pair list, symbols
+  const int wl = ((PV_K + 1) * rss + PV_K * rs + rs + 64 + (rs + 64) / 2 + rs / 2 + lcap / 4 + 32 + 1) & ~1;
   const int shared = n * rsa + rs;
   const int budget = 160 * 1024 / 8 - shared;
-  const int waves = std::min(8, budget / wl);
+  const int waves = std::min(ns == 1 ? 8 : 4, budget / wl);  // (the launch bounds)
   if (waves < 1) return g;
   g.ns = ns;
   g.waves = waves;

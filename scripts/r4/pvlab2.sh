@@ -7,5 +7,5 @@ timeout -k 10 300 env ITR_PV=1 python -u -m pytest tests/test_gpu_sweeps.py test
 tail -1 $O/pytest.log
 timeout -k 10 200 env ITR_LIB=itrails_amd/libitrails_hip_diag.so ITR_PV=1 python scripts/pv_lab.py lone long chr10 > $O/diag.txt 2>&1 || { tail -20 $O/diag.txt; exit 1; }
 cat $O/diag.txt
-timeout -k 10 200 ITR_PV=1 python scripts/pv_lab.py lone long chr10 > $O/prod.txt 2>&1 || { tail -20 $O/prod.txt; exit 1; }
+timeout -k 10 200 env ITR_PV=1 python scripts/pv_lab.py lone long chr10 > $O/prod.txt 2>&1 || { tail -20 $O/prod.txt; exit 1; }
 cat $O/prod.txt
