@@ -244,10 +244,11 @@ struct itr_model {
   // (row 625), when that layout serves this state count (wave_tasks.h)
   double* EF = nullptr;
   int erf = 0;
-  // the prediction-and-verification Viterbi (pv_viterbi.hip): log a^T with a -inf diagonal
-  // (rows padded to rsa with -inf), log a_jj, max_{i != j} log a_ij, and log E padded to xe
-  // columns (-inf), when that layout serves this state count
+  // the prediction-and-verification Viterbi (pv_viterbi.hip): log a^T (rows padded to rsa
+  // with -inf), log a_jj, max_{i != j} log a_ij, and log E padded to xe columns (-inf), when
+  // that layout serves this state count
   double *LAT = nullptr, *LDG = nullptr, *LMJ = nullptr, *LEP = nullptr;
+  bool pv_safe = true;  // some omega can be -inf: a zero in pi E or E, or an unreachable state
 };
 
 struct itr_plan {
@@ -666,15 +667,20 @@ int itr_model_create(int n, const double* a, const double* la, const double* E,
     for (int i = 0; i < n; ++i)
       for (int j = 0; j < n; ++j) {
         const double v = la[(size_t)i * n + j];
-        if (i == j) {
+        lat[(size_t)j * pg.rsa + i] = v;
+        if (i == j)
           ldg[j] = v;
-        } else {
-          lat[(size_t)j * pg.rsa + i] = v;
+        else
           lmj[j] = std::max(lmj[j], v);
-        }
       }
+    bool inf = false;
     for (int o = 0; o < ITR_NOBS; ++o)
-      for (int j = 0; j < n; ++j) lep[(size_t)o * pg.xe + j] = LE[(size_t)o * n + j];
+      for (int j = 0; j < n; ++j) {
+        lep[(size_t)o * pg.xe + j] = LE[(size_t)o * n + j];
+        inf = inf || !(LE[(size_t)o * n + j] > -INFINITY) || !(LPIE[(size_t)o * n + j] > -INFINITY);
+      }
+    for (int j = 0; j < n && !inf; ++j) inf = !(lmj[j] > -INFINITY) && !(ldg[j] > -INFINITY);
+    m->pv_safe = inf;
     double** dst2[4] = {&m->LAT, &m->LDG, &m->LMJ, &m->LEP};
     const std::vector<double>* src2[4] = {&lat, &ldg, &lmj, &lep};
     for (int i = 0; i < 4 && !e; ++i) {
@@ -1175,6 +1181,7 @@ int pv_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path, hip
   a.ckpt = p->d_alpha;
   a.stay = p->d_stay;
   a.last_state = p->d_last;
+  a.safe = m->pv_safe ? 1 : 0;
   const int cus = cu_count();
   // the ~CU-count longest blocks at raised wave priority against the co-resident waves
   a.prio_len = (int)std::max<int64_t>(

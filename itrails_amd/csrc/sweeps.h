@@ -156,7 +156,7 @@ struct PvArgs {
   const int64_t* off;           // [plan blocks + 1]
   const int64_t* tile_off;      // [plan blocks + 1]
   const uint16_t* obs;          // [total]
-  const double* lat;            // log a^T with -inf diagonal and padding: n x rsa
+  const double* lat;            // log a^T with -inf padding: n x rsa
   const double* ldg;            // [n] log a_jj
   const double* lmj;            // [n] max_{i != j} log a_ij
   const double* lep;            // log E padded to xe columns (-inf): 625 x xe
@@ -165,6 +165,7 @@ struct PvArgs {
   uint16_t* stay;               // [tiles x xr]
   uint8_t* last_state;          // [plan blocks]
   int prio_len;                 // blocks at least this long run at raised wave priority
+  int safe;                     // some omega can be -inf (model with zero probabilities)
   uint64_t* diag;               // diagnostic build only: event counts and phase cycles
   // layout (set by launch_pv_vit from the geometry)
   int rsa, rs, rss, xe, eb, lcap, wl;
