@@ -300,8 +300,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=["auto", "chr10", "chr100"], default="auto")
     ap.add_argument("--n-int", type=int, default=5)
-    ap.add_argument("--mode", choices=["fv", "posterior", "optimize"], default="fv",
+    ap.add_argument("--mode", choices=["fv", "vit", "posterior", "optimize"], default="fv",
                     help="fv: forward + Viterbi (BASELINE configs 2 and 4, the default); "
+                         "vit: Viterbi decoding alone (the itrails-viterbi / viterbi_wrapper "
+                         "call); "
                          "posterior: posterior decoding (config 3, use --n-int 7); optimize: "
                          "one itrails-optimize objective evaluation per step = device model "
                          "rebuild + forward log-likelihood of the resident columns (config 5)")
@@ -385,6 +387,7 @@ def main():
     plan = hmm.Plan(off)
     post_mode = args.mode == "posterior"
     opt_mode = args.mode == "optimize"
+    vit_mode = args.mode == "vit"
     plan.reserve(n, posterior=post_mode)
     d_obs = torch.from_numpy(obs.astype(np.int16)).to(dev)
     d_ll = torch.empty(plan.nblocks, dtype=torch.float64, device=dev)
@@ -443,6 +446,13 @@ def main():
             if timing:
                 fwd_ms.append(hmm.last_kernel_ms("posterior_fwd"))
                 vit_ms.append(hmm.last_kernel_ms("posterior_bwd"))
+            return
+        if vit_mode:  # itr_viterbi: sweep + traceback, the path returned to the caller
+            hmm.viterbi_device(model, plan, d_obs, out=d_path)
+            if timing:
+                vit_ms.append(hmm.last_kernel_ms("viterbi"))
+                tb_ms.append(hmm.last_kernel_ms("traceback"))
+            torch.cuda.current_stream().synchronize()
             return
         if args.overlap and not timing:
             # forward + Viterbi in one call (itr_forward_viterbi): the forward sweep runs
@@ -523,7 +533,9 @@ def main():
     # checks against the CPU restatement, every rank on its own blocks
     threads = host_threads()
     check = None
-    if args.verify and args.mode == "fv":
+    if args.verify and args.mode in ("fv", "vit"):
+        if vit_mode:  # (the log-likelihoods for the check only)
+            hmm.forward_loglik_device(model, plan, d_obs, out=d_ll)
         c = oracle_check_fv(a, b, pi, obs, off, d_ll.cpu().numpy(), d_path.cpu().numpy(), threads)
         check = {"loglik_max_rel_err": allreduce(c["max_rel"], "max"),
                  "loglik_total_rel_err": allreduce(c["total_rel"], "max"),
@@ -559,12 +571,23 @@ def main():
         tb_avg = float(np.mean(tb_ms)) if tb_ms else 0.0
         pair_ops = 2.0 * n * n  # per column: N^2 FMA (forward / backward) or N^2 add + N^2 max
         step_ms = dt / args.steps * 1e3
+        fv_avg = float(np.mean(fv_ms)) if fv_ms else 0.0
         if args.mode == "fv":
-            dom, dom_ms, dom_peak, dom_mode = ("Viterbi max-plus sweep: sweep_kernel<VIT> (longest "
-                                               "blocks, reserved CUs) | wave_vit_kernel (rest)"), \
-                vit_avg, am_peak, 3
+            # the timed call itself (itr_forward_viterbi, fork to join): its ideal time at
+            # the VALU peaks, forward at the FMA rate and Viterbi at the add+max rate
             ideal_ms = pair_ops * cols_local / (fma_peak * 1e12) * 1e3 + \
                 pair_ops * cols_local / (am_peak * 1e12) * 1e3
+            dom = ("itr_forward_viterbi: hybrid_sweep_kernel<FWD_LL> (forward VALU halves, "
+                   "reserved CUs) | sweep_kernel<VIT> (longest blocks, reserved CUs) | "
+                   "wave_mixed_kernel (forward groups + per-wave Viterbi, the rest)")
+            dom_ms = fv_avg if fv_avg else vit_avg
+            dom_peak = 2 * pair_ops * cols_local / (ideal_ms * 1e-3) / 1e12  # combined peak
+            dom_mode = 3
+        elif vit_mode:
+            dom, dom_ms, dom_peak, dom_mode = ("Viterbi max-plus sweep: sweep_kernel<VIT> (longest "
+                                               "blocks, both reserved CU sets) | wave_vit_kernel "
+                                               "(rest)"), vit_avg, am_peak, 3
+            ideal_ms = pair_ops * cols_local / (am_peak * 1e12) * 1e3
         elif post_mode:
             dom, dom_ms, dom_peak, dom_mode = "sweep_kernel<BWD> (backward + posterior)", vit_avg, \
                 fma_peak, 2
@@ -573,7 +596,8 @@ def main():
             dom, dom_ms, dom_peak, dom_mode = "sweep_kernel<FWD_LL> (forward)", fwd_avg, \
                 fma_peak, 0
             ideal_ms = pair_ops * cols_local / (fma_peak * 1e12) * 1e3
-        achieved = pair_ops * cols_local / (dom_ms * 1e-3) / 1e12 if dom_ms else 0.0
+        dom_ops = (2 if args.mode == "fv" else 1) * pair_ops * cols_local
+        achieved = dom_ops / (dom_ms * 1e-3) / 1e12 if dom_ms else 0.0
         traffic, traffic_note = pmc_traffic(n, dom_mode)
         rates, rates_src = pmc_rates(n)
         cpu = None
@@ -607,6 +631,7 @@ def main():
                              "threads (OMP_NUM_THREADS = this job's CPU share)",
                    "one_core": one}
         metric = {"fv": "alignment columns/s (forward+Viterbi), 3sp+outgroup HMM",
+                  "vit": "alignment columns/s (Viterbi decoding), 3sp+outgroup HMM",
                   "posterior": "alignment columns/s (posterior decoding), 3sp+outgroup HMM",
                   "optimize": "itrails-optimize objective evaluations/s (device model rebuild "
                               "+ forward loglik of the resident alignment)"}[args.mode]
@@ -634,6 +659,7 @@ def main():
                                    ("alignment sharded over the ranks" if W["scaling"] == "strong"
                                     else "per GPU") + f", {args.n_int}+{args.n_int} intervals, " +
                                    {"fv": "forward loglik + Viterbi traceback",
+                                    "vit": "Viterbi sweep + traceback",
                                     "posterior": "posterior decoding",
                                     "optimize": "model rebuild + forward loglik per "
                                                 "evaluation"}[args.mode],
@@ -645,8 +671,9 @@ def main():
                        "world_size_seen": seen_world,
                        "backend": (dist.get_backend() if world > 1 else None)},
             "roofline": {"kernel": dom, "bound": "valu",
-                         "pipe": "FP64 VALU (add+max pairs)" if args.mode == "fv" else
-                                 "FP64 VALU FMA",
+                         "pipe": {"fv": "FP64 VALU (forward FMA + Viterbi add+max pairs)",
+                                  "vit": "FP64 VALU (add+max pairs)"}.get(args.mode,
+                                                                        "FP64 VALU FMA"),
                          "achieved": round(achieved, 4), "peak": round(dom_peak, 3),
                          "unit": "TFLOP/s", "frac": round(achieved / dom_peak, 5),
                          "peak_source": peak_src,
@@ -656,8 +683,8 @@ def main():
                          "traffic": traffic, "traffic_note": traffic_note,
                          "kernel_ms": round(dom_ms, 4),
                          "forward_ms": round(fwd_avg, 4),
-                         "viterbi_ms": round(vit_avg, 4) if args.mode == "fv" else None,
-                         "traceback_ms": round(tb_avg, 4) if args.mode == "fv" else None,
+                         "viterbi_ms": round(vit_avg, 4) if args.mode in ("fv", "vit") else None,
+                         "traceback_ms": round(tb_avg, 4) if args.mode in ("fv", "vit") else None,
                          "forward_viterbi_ms": round(float(np.mean(fv_ms)), 4) if fv_ms else None,
                          "algorithmic": f"{pair_ops:.0f} FP64 ops/column per sweep x "
                                         f"{cols_local} columns (rank 0)",
@@ -670,7 +697,7 @@ def main():
                 "allreduce_bytes": int(d_ll_global.numel() * 8)} if world > 1 else {}),
             **({"host_path": host} if host is not None else {}),
             **(check or {}),
-            "loglik_total": ll_total if args.mode != "posterior" else None,
+            "loglik_total": ll_total if args.mode not in ("posterior", "vit") else None,
             "gen_seconds": round(gen_s, 2),
         }
         print(json.dumps(result), flush=True)

@@ -288,6 +288,7 @@ struct itr_plan {
   // Viterbi blocks, < 0 = forward groups of groups_ll, by expected duration; tasks at least
   // mix_prio_* long run at raised wave priority
   int64_t vit_nlong = 0, vit_long_cols = 0, nmix = 0;
+  int64_t vit_nlong_v = 0;  // the Viterbi-only call's long set (plan_partition)
   // CU partition (plan_partition): reserved CUs for the long blocks' Viterbi and for the
   // forward's VALU halves; wave_ok = false when the long work cannot fit half the chip
   int vit_reserve = 0, fwd_reserve = 0;
@@ -342,7 +343,14 @@ int vit_stride(int n) {
 //               (calibrated on chr10: 0.15 / 0.165 / 0.18 / 0.195 us -> forward+Viterbi call
 //               8.52 / 8.49 / 8.29-8.69 / 8.41-8.56 ms, profiles/r3ab5_partition.txt)
 //   kFwdValu    a forward VALU half alone on its CU                            370 ns / column
-constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kBulkCu = 180e-9, kFwdValu = 370e-9;
+//   kBulkVit    Viterbi alone of a column in the per-wave launch               115 CU-ns / column
+//               (10 M columns of short blocks in 4.43 ms on 256 CUs)
+//   kVitWaveLatV  a per-wave Viterbi block's step in that launch under full    700 ns / column
+//               load (two waves per SIMD: ~640 ns alone), calibrated on the chr10 Viterbi-only
+//               call with 0 / 30 / 59 / 80 / 100 / 124 long blocks: 12.1 / 6.42 / 5.76 / 5.80 /
+//               6.02 / 7.97 ms (profiles/r4m_vit_long_set.txt; this rule picks 69)
+constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kBulkCu = 180e-9, kFwdValu = 370e-9,
+                 kBulkVit = 115e-9, kVitWaveLatV = 700e-9;
 
 // Bins of capacity `cap` (first fit, items longest first): the CUs a set of sequential tasks
 // needs to finish within cap
@@ -392,6 +400,17 @@ void plan_partition(itr_plan_t p, const std::vector<int64_t>& ulen, int cus) {
   p->fwd_reserve = rf;  // (viterbi_impl rounds both up to whole XCC sets)
   p->vit_reserve = rv;
   p->wave_ok = rv + rf <= cus / 2;
+  // the Viterbi-only call (itr_viterbi) on the same two reserved sets: its own makespan (the
+  // per-wave Viterbi's bulk cost, no forward) decides its long set, which both reserved sets
+  // sweep before they join the bulk
+  const double Tv = std::max((double)p->total * kBulkVit / cus, tmax * kVitLone);
+  int64_t kv = 0;
+  while (kv < nblocks && p->sorted_len[kv] >= 2048 && (double)p->sorted_len[kv] * kVitWaveLatV > Tv)
+    ++kv;
+  p->vit_nlong_v = kv;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_VIT_NLONG_V")) p->vit_nlong_v = atoi(getenv("ITR_VIT_NLONG_V"));
+#endif
   if (getenv("ITR_VERBOSE"))
     fprintf(stderr, "[itr] partition: T %.3f ms, long %lld blocks (%lld cols), rv %d rf %d (%zu halves)%s\n",
             T * 1e3, (long long)k, (long long)cols, p->vit_reserve, rf, halves.size(),
@@ -465,7 +484,7 @@ uint64_t* g_diag = nullptr;  // diagnostic build: per-segment cycle sums of the 
 // tname: kernel timer (nullptr: none); max_grid > 0 caps the persistent grid
 // cus: the CUs the launch's stream may use (default: all)
 int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
-              int64_t max_grid = -1, int cus = 0) {
+              int64_t max_grid = -1, int cus = 0, bool zero_queue = true) {
   itr::SweepGeometry g = itr::sweep_geometry(a.n, mode);
   if (g.iq < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", a.n);
   a.xp = g.xp;
@@ -475,7 +494,7 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
   if (max_grid > 0 && grid > max_grid) grid = max_grid;
   if (grid <= 0) return 0;
   if (grid <= cus) g.lds = std::max(g.lds, itr::kExclusiveLds);  // one per CU
-  HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
+  if (zero_queue) HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
 #ifdef ITR_DIAG
   if (getenv("ITR_VERBOSE"))
     fprintf(stderr, "[itr] %s: n=%d cfg=%d block=%d lds=%zu per_cu=%d grid=%lld\n", tname, a.n,
@@ -1264,7 +1283,23 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   bool wave = wv.iq > 0 && m->LEW && m->xrw == wv.xr;
   const int cus = cu_count();
   if (wave && !p->wave_ok) wave = false;  // the long work would need more than half the CUs
-  const int64_t nlong = wave ? p->vit_nlong : 0;
+  // the reserved CU sets (plan_partition: sized for the forward+Viterbi call; the
+  // Viterbi-only call runs on the same CU-masked streams, with its own long set swept by
+  // both sets)
+  const int64_t nlong_c = wave ? p->vit_nlong : 0;
+  const int64_t rf0 = p->fwd_reserve;
+  const int64_t rv0 = nlong_c > 0 ? std::max(1, p->vit_reserve) : 0;
+  // whole XCC sets: a mask that leaves an XCC without a reserved CU does not mask it at all
+  const int X = (cus % 8 == 0) ? 8 : 1;
+  int Xr = X;  // rounding unit of the reserved sets
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_SE_ROUND")) Xr = 4 * X;  // one CU per shader engine
+#endif
+  const int rvr = (int)std::min<int64_t>((rv0 + Xr - 1) / Xr * Xr, cus / 2);
+  const int rfr = (int)std::min<int64_t>((rf0 + Xr - 1) / Xr * Xr, cus / 4);
+  const int reserve_cus = rvr + rfr;
+  const bool vonly = fwd_loglik == nullptr;
+  const int64_t nlong = vonly ? (wave && reserve_cus > 0 ? p->vit_nlong_v : 0) : nlong_c;
   // Few blocks, all long (e.g. 100 blocks of 100 kbp): one CU per block for the 9-wave
   // Viterbi sweep and the forward sweep beside it on the remaining CUs (at least a quarter
   // of the chip), instead of one after the other
@@ -1335,18 +1370,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     af.svec = p->d_svec;
     af.sK = p->d_sK;
     // (the forward's reserved set exists without the forward too — one partition, one set
-    // of streams per plan — and then runs bulk blocks from the start)
-    const int64_t rf = p->fwd_reserve;
-    const int64_t rv = nlong > 0 ? std::max(1, p->vit_reserve) : 0;
-    // whole XCC sets: a mask that leaves an XCC without a reserved CU does not mask it at all
-    const int X = (cus % 8 == 0) ? 8 : 1;
-    int Xr = X;  // rounding unit of the reserved sets
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_SE_ROUND")) Xr = 4 * X;  // one CU per shader engine
-#endif
-    const int rvr = (int)std::min<int64_t>((rv + Xr - 1) / Xr * Xr, cus / 2);
-    const int rfr = (int)std::min<int64_t>((rf + Xr - 1) / Xr * Xr, cus / 4);
-    const int reserve_cus = rvr + rfr;
+    // of streams per plan; the Viterbi-only call sweeps its long set on it too)
     if (split_fwd) {
       HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
       HIP_TRY(hipMemsetAsync(p->d_queue + 8, 0, 2 * sizeof(int), st));  // the idle loops' counters
@@ -1354,6 +1378,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     // before the fork: the bulk queue is shared with the reserved CUs' late launch
     HIP_TRY(hipMemsetAsync(mixed ? p->d_queue + 12 : w.queue, 0, sizeof(int), st));
     if (nlong > 0) HIP_TRY(hipMemsetAsync(p->d_queue + 13, 0, sizeof(int), st));
+    if (nlong > 0 && vonly) HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
     if (reserve_cus > 0) {
       // the long blocks' Viterbi on lng (rvr CUs), the forward's VALU halves on lng2 (rfr
       // others): separate masks, so each set joins the bulk queue as soon as its own long
@@ -1362,7 +1387,8 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       HIP_TRY(hipEventRecord(pt->fork, st));
       HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
       HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
-      if (nlong > 0) {
+      HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
+      if (nlong > 0 && !vonly) {
         a.nblocks = nlong;
         if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, rvr)) return e;
         itr::TraceArgs tl = trace_args();
@@ -1372,8 +1398,13 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
         HIP_TRY(itr::launch_vit_traceback(tl, (int)std::min<int64_t>((nlong + 3) / 4, 4 * rvr),
                                           pt->lng));
         traced = nlong;
+      } else if (nlong > 0) {  // Viterbi alone: both reserved sets sweep the long set
+        a.nblocks = nlong;
+        if (rvr > 0)
+          if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, rvr, 0, false)) return e;
+        if (rfr > 0)
+          if (int e = run_sweep(itr::MODE_VIT, a, pt->lng2, nullptr, rfr, 0, false)) return e;
       }
-      HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
       if (split_fwd) {
         if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, pt->lng2, nullptr, true, false,
                                rfr, false))
@@ -1412,10 +1443,10 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       if (pt) {  // the reserved CUs join the bulk queue when their long work is done
         if (rvr > 0)
           HIP_TRY(itr::launch_wave_mixed(wf, wf.mixed_per_cu * rvr, w, f, p->d_mix,
-                                         (int)p->nmix, p->d_queue + 12, pt->lng));
+                                         (int)p->nmix, p->d_queue + 12, pt->lng, 1));
         if (rfr > 0)
           HIP_TRY(itr::launch_wave_mixed(wf, wf.mixed_per_cu * rfr, w, f, p->d_mix,
-                                         (int)p->nmix, p->d_queue + 12, pt->lng2));
+                                         (int)p->nmix, p->d_queue + 12, pt->lng2, 2));
       }
     } else {
       if (split_fwd) {
@@ -1429,9 +1460,9 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
         const int64_t grid = std::min<int64_t>((int64_t)wv.per_cu * ocus, (w.nblocks + 3) / 4);
         HIP_TRY(itr::launch_wave_vit(wv, (int)grid, w, sb));
         if (pt && rvr > 0)  // the reserved CUs join when their long work is done
-          HIP_TRY(itr::launch_wave_vit(wv, wv.per_cu * rvr, w, pt->lng));
+          HIP_TRY(itr::launch_wave_vit(wv, wv.per_cu * rvr, w, pt->lng, 1));
         if (pt && rfr > 0)
-          HIP_TRY(itr::launch_wave_vit(wv, wv.per_cu * rfr, w, pt->lng2));
+          HIP_TRY(itr::launch_wave_vit(wv, wv.per_cu * rfr, w, pt->lng2, 2));
       }
     }
     if (pt) {

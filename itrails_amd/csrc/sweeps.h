@@ -142,8 +142,9 @@ struct WaveVitGeometry {
   int per_cu;   // resident workgroups per CU
 };
 WaveVitGeometry wave_vit_geometry(int n);
+// role: 0 = bulk launch, 1 / 2 = a reserved set's late launch (only the kernel name differs)
 hipError_t launch_wave_vit(const WaveVitGeometry& g, int grid, const VitArgs& p,
-                           hipStream_t st);
+                           hipStream_t st, int role = 0);
 
 // Viterbi by prediction and verification (pv_viterbi.hip): one block per wavefront, the
 // workgroup's waves sharing log a in LDS; same outputs as MODE_VIT
@@ -224,7 +225,7 @@ hipError_t launch_wave_mfma(const WaveMfmaGeometry& g, int grid, const WaveMfmaA
 // Viterbi block e (v), e < 0 = forward group -e - 1 (f); queue zero at launch
 hipError_t launch_wave_mixed(const WaveMfmaGeometry& g, int grid, const VitArgs& v,
                              const WaveMfmaArgs& f, const int32_t* list, int nlist, int* queue,
-                             hipStream_t st);
+                             hipStream_t st, int role = 0);
 
 // log-likelihoods of the split blocks of a forward sweep
 hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,

@@ -22,7 +22,9 @@ __device__ __forceinline__ int next_task(int* queue) {
   return uni(atomicAdd(queue, (threadIdx.x & 63) == 0 ? 1 : 0));
 }
 
-template <int IQ>
+// ROLE only names the launch in kernel traces: 0 = the bulk launch, 1 / 2 = the late launches
+// of the reserved CU sets joining the same queue (same code)
+template <int IQ, int ROLE>
 __global__ void __launch_bounds__(64 * kWaves, 2) wave_vit_kernel(VitArgs p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* wl = reinterpret_cast<double*>(smem) + (size_t)(threadIdx.x >> 6) * WaveVit<IQ>::WL;
@@ -51,7 +53,7 @@ template <int IQ, int NT, int NK>
 struct Mixed {
   static constexpr int WL = WaveVit<IQ>::WL > WF<NT, NK>::WL ? WaveVit<IQ>::WL : WF<NT, NK>::WL;
 };
-template <int IQ, int NT, int NK>
+template <int IQ, int NT, int NK, int ROLE>
 __global__ void __launch_bounds__(64 * kWaves, 2)
     wave_mixed_kernel(VitArgs v, WaveMfmaArgs f, const int32_t* list, int nlist, int* queue) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -98,17 +100,17 @@ WaveVitGeometry wave_vit_geometry(int n) {
   g.block = 64 * kWaves;
   g.xr = 8 * g.iq;
   g.lds = (size_t)kWaves * WaveVit<9>::WL * sizeof(double);
-  g.per_cu = occupancy(wave_vit_kernel<9>, g.lds);
+  g.per_cu = occupancy(wave_vit_kernel<9, 0>, g.lds);
   return g;
 }
 
 hipError_t launch_wave_vit(const WaveVitGeometry& g, int grid, const VitArgs& p,
-                           hipStream_t st) {
-  switch (g.iq) {
-    case 9:
-      hipLaunchKernelGGL(wave_vit_kernel<9>, dim3(grid), dim3(g.block), g.lds, st, p);
-      break;
-    default: return hipErrorInvalidValue;
+                           hipStream_t st, int role) {
+  if (g.iq != 9) return hipErrorInvalidValue;
+  switch (role) {
+    case 0: hipLaunchKernelGGL((wave_vit_kernel<9, 0>), dim3(grid), dim3(g.block), g.lds, st, p); break;
+    case 1: hipLaunchKernelGGL((wave_vit_kernel<9, 1>), dim3(grid), dim3(g.block), g.lds, st, p); break;
+    default: hipLaunchKernelGGL((wave_vit_kernel<9, 2>), dim3(grid), dim3(g.block), g.lds, st, p); break;
   }
   return hipGetLastError();
 }
@@ -132,7 +134,7 @@ WaveMfmaGeometry wave_mfma_geometry(int n) {
   g.mixed = (n > 64 && n <= 72) && g.cfg == 2;
   if (g.mixed) {
     g.mixed_lds = (size_t)kWaves * Mixed<9, 5, 18>::WL * sizeof(double);
-    g.mixed_per_cu = occupancy(wave_mixed_kernel<9, 5, 18>, g.mixed_lds);
+    g.mixed_per_cu = occupancy(wave_mixed_kernel<9, 5, 18, 0>, g.mixed_lds);
   }
   return g;
 }
@@ -155,10 +157,22 @@ hipError_t launch_wave_mfma(const WaveMfmaGeometry& g, int grid, const WaveMfmaA
 
 hipError_t launch_wave_mixed(const WaveMfmaGeometry& g, int grid, const VitArgs& v,
                              const WaveMfmaArgs& f, const int32_t* list, int nlist, int* queue,
-                             hipStream_t st) {
+                             hipStream_t st, int role) {
   if (!g.mixed) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((wave_mixed_kernel<9, 5, 18>), dim3(grid), dim3(g.block), g.mixed_lds, st,
-                     v, f, list, nlist, queue);
+  switch (role) {
+    case 0:
+      hipLaunchKernelGGL((wave_mixed_kernel<9, 5, 18, 0>), dim3(grid), dim3(g.block), g.mixed_lds,
+                         st, v, f, list, nlist, queue);
+      break;
+    case 1:
+      hipLaunchKernelGGL((wave_mixed_kernel<9, 5, 18, 1>), dim3(grid), dim3(g.block), g.mixed_lds,
+                         st, v, f, list, nlist, queue);
+      break;
+    default:
+      hipLaunchKernelGGL((wave_mixed_kernel<9, 5, 18, 2>), dim3(grid), dim3(g.block), g.mixed_lds,
+                         st, v, f, list, nlist, queue);
+      break;
+  }
   return hipGetLastError();
 }
 

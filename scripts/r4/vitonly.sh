@@ -1,0 +1,16 @@
+# Round 4: Viterbi-only partition + timed-call roofline: sweep/full-size tests, fv and vit
+# bench lines, kernel trace of the fv bench
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-r4l}
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_sweeps.py tests/test_gpu_fullsize.py -x -q -m gpu --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+B="--cpu-1core-cols 0 --host-path 0"
+timeout -k 10 300 python bench.py $B > $O/fv.json 2> $O/fv.err || { tail $O/fv.err; exit 1; }
+python scripts/bench_line.py $O/fv.json chr10
+timeout -k 10 300 python bench.py $B --mode vit > $O/vit.json 2> $O/vit.err || { tail $O/vit.err; exit 1; }
+python scripts/bench_line.py $O/vit.json vit
+P="python3 bench.py --steps 3 --warmup 1 --verify 0 $B"
+timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $O/prof -o trace --output-format csv -- $P > $O/prof_trace.log 2>&1 || { tail $O/prof_trace.log; exit 1; }
+echo done
