@@ -330,6 +330,10 @@ def main():
     ap.add_argument("--split-build", type=int, default=1, choices=[0, 1],
                     help="optimize mode, N > 1: divide each rebuild's Van Loan work over the "
                          "ranks (one RCCL all-gather) instead of rebuilding on every rank")
+    ap.add_argument("--project-shards", type=int, default=0,
+                    help="chr100 at N = 1 only: also time each of the W shards a W-GPU run "
+                         "would get, alone on this GPU, and report the projected speed-up "
+                         "(the N = 1 step / the slowest shard's step)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the exchange with several ranks on one GPU)")
@@ -554,6 +558,34 @@ def main():
                  "columns_checked": int(allreduce(c["cols"], "sum")),
                  "row_sum_max_abs_dev_all_columns": allreduce(sums, "max")}
 
+    # each shard of a W-way split alone on this GPU (chr100, N = 1): the strong-scaling
+    # projection of BASELINE config 4 without an 8-GPU node
+    shards = None
+    if args.project_shards > 1 and kind == "chr100" and world == 1 and args.mode == "fv":
+        per = []
+        for r in range(args.project_shards):
+            Ws = make_workload(kind, a, b, pi, r, args.project_shards, args.mean_block, args.mbp,
+                               args.block_len)
+            sp = hmm.Plan(Ws["off"])
+            sp.reserve(n)
+            so = torch.from_numpy(Ws["obs"].astype(np.int16)).to(dev)
+            for _ in range(args.warmup):
+                hmm.forward_viterbi_device(model, sp, so)
+            torch.cuda.synchronize()
+            ts = time.perf_counter()
+            for _ in range(args.steps):
+                hmm.forward_viterbi_device(model, sp, so)
+                torch.cuda.current_stream().synchronize()
+            per.append(round((time.perf_counter() - ts) / args.steps * 1e3, 4))
+            del so
+            sp.close()
+        step_n1 = dt / args.steps * 1e3
+        shards = {"world": args.project_shards, "per_shard_ms": per, "max_ms": max(per),
+                  "slowest_rank": int(np.argmax(per)), "n1_step_ms": round(step_n1, 4),
+                  "projected_speedup": round(step_n1 / max(per), 3),
+                  "note": "each shard's itr_forward_viterbi step alone on this one GPU "
+                          "(RCCL all-reduce of the per-block log-likelihoods not included)"}
+
     # the drop-in call from host buffers (N = 1), resident benchmark buffers released first
     host = None
     if args.host_path and not opt_mode and world == 1:
@@ -696,6 +728,7 @@ def main():
             **({"per_rank_step_ms": per_rank_ms, "allreduce_ms": xchg_ms,
                 "allreduce_bytes": int(d_ll_global.numel() * 8)} if world > 1 else {}),
             **({"host_path": host} if host is not None else {}),
+            **({"shard_projection": shards} if shards is not None else {}),
             **(check or {}),
             "loglik_total": ll_total if args.mode not in ("posterior", "vit") else None,
             "gen_seconds": round(gen_s, 2),

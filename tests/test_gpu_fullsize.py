@@ -9,8 +9,9 @@ do not need the CPU oracle to run over all of it:
     creation): the same value to 1e-12 relative;
   * the combined call the bench times (itr_forward_viterbi: the CU-partitioned forward +
     Viterbi) against the oracle on EVERY block: paths identical, log-likelihoods 1e-8; and
-    the same on BASELINE config 4's rank-0 shard at world size 8 (the chr100 layout, which
-    takes the other branches of the partition);
+    the same on every one of BASELINE config 4's eight shards at world size 8 (the chr100
+    layout, which takes the other branches of the partition);
+  * the device-built (5,5) model against the reference-built one on the whole workload;
   * every block's log-likelihood finite and negative, the total equal to the block-order
     sum of the per-block values (loglik_wrapper semantics);
   * every posterior row sums to 1 (1e-12) and matches the oracle on the sampled blocks.
@@ -100,25 +101,55 @@ def test_full_size_forward_viterbi_every_block(full):
     _check_all_blocks(full["t"], full["obs"], full["off"], ll, path)
 
 
-def test_chr100_rank0_shard_forward_viterbi(gpu):
-    """BASELINE config 4's per-rank work at world size 8: the rank-0 shard of the fixed
-    100 Mbp alignment (bench.py --workload chr100: shard_ranges over the geometric block
-    layout, ~12.5 Mbp) through itr_forward_viterbi, every block against the oracle."""
+@pytest.mark.parametrize("rank", range(8))
+def test_chr100_shard_forward_viterbi(gpu, rank):
+    """BASELINE config 4's per-rank work at world size 8: every shard of the fixed 100 Mbp
+    alignment (bench.py --workload chr100: shard_ranges over the geometric block layout,
+    ~12.5 Mbp each; rank 3 holds the alignment's longest block, 23,881 columns) through
+    itr_forward_viterbi, every block against the oracle."""
     import torch
     from itrails_amd.distributed import shard_ranges
     from itrails_amd.synth import sample_alignment_range
     g = golden("model_kat_5_5.npz")
     a, b, pi = g["a"], g["b"], g["pi"]
     lengths = block_lengths(np.random.default_rng(12345), 100_000_000, 2000.0)
-    lo, hi = shard_ranges(lengths, 8)[0]
+    lo, hi = shard_ranges(lengths, 8)[rank]
     obs, off = sample_alignment_range(a, b, pi, lengths, lo, hi, seed=777)
     assert 11_000_000 < off[-1] < 14_000_000
+    if rank == 3:
+        assert np.diff(off).max() == lengths.max() == 23881
     model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
     d_obs = torch.from_numpy(obs.astype(np.int16)).cuda()
     ll, path = hmm.forward_viterbi_device(model, plan, d_obs)
     _check_all_blocks(build_tables(a, b, pi), obs, off, ll.cpu().numpy(), path.cpu().numpy())
     del d_obs, plan
     torch.cuda.empty_cache()
+
+
+def test_device_built_vs_reference_model_decode(full):
+    """config 2 decoded with the (5,5) model the drop-in CLIs build on the
+    device (model.trans_emiss_calc, KAT parameters) instead of the reference-built one
+    (tests/golden/model_kat_5_5.npz).  The two models agree to ~1e-15 (a, pi) / 1e-8 (b);
+    the log-likelihoods agree within 1e-8 relative; the number of Viterbi columns that differ
+    is recorded, not asserted zero: a near-tie decided by the last bit can
+    flip."""
+    import json
+    from itrails_amd.model import trans_emiss_calc
+    from itrails_amd.model.linalg import DeviceLinalg
+    g = golden("model_kat_5_5.npz")
+    n_ab, n_abc = (int(x) for x in g["n_int"])
+    a, b, pi, _, _ = trans_emiss_calc(*g["args"], n_ab, n_abc, la=DeviceLinalg())
+    model = hmm.Model(a, b, pi)
+    plan = hmm.Plan(full["off"])
+    ll, path = hmm.forward_viterbi_device(model, plan, full["d_obs"])
+    ll, path = ll.cpu().numpy(), path.cpu().numpy()
+    np.testing.assert_allclose(ll, full["ll"], rtol=1e-8, atol=0)
+    diff = int((path != full["path"]).sum())
+    rel = float(np.max(np.abs(ll - full["ll"]) / np.abs(full["ll"])))
+    print(json.dumps({"viterbi_columns_differing": diff, "columns": int(full["off"][-1]),
+                      "loglik_max_rel_diff": rel, "a_max_abs_diff": float(np.abs(a - g["a"]).max()),
+                      "b_max_abs_diff": float(np.abs(b - g["b"]).max())}))
+    assert diff <= 1000  # (observed: see DESIGN.md §7)
 
 
 def test_full_size_loglik_properties(full):

@@ -182,3 +182,31 @@ def test_forward_viterbi_call_matches_separate_calls(gpu, n):
     np.testing.assert_array_equal(p2, p1)
     np.testing.assert_array_equal(p2, O.viterbi(t, obs, off))
     np.testing.assert_allclose(ll2, O.forward_loglik(t, obs, off), rtol=RTOL, atol=0)
+
+
+@pytest.mark.parametrize("n", [46, 70, 133])
+def test_few_long_blocks_forward_viterbi(gpu, n):
+    """The few-block branch of itr_forward_viterbi (capi.cpp viterbi_impl `few`: no more
+    blocks than 3/4 of the CUs and no per-wave layout, e.g. 100 x 100 kbp): the Viterbi sweep
+    on a masked set of CUs, one per block, the forward on the others at the same time.  96
+    equally long blocks of 5,000 columns (every block in the long set, so the partition's
+    long work exceeds half the chip and the per-wave layout is off at n = 70 too): the
+    combined call against the separate calls (paths bit for bit, log-likelihoods 1e-12) and
+    against the oracle."""
+    import torch
+
+    rng = np.random.default_rng(90 + n)
+    a, b, pi = random_hmm(rng, n)
+    lengths = [5000] * 96
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=n, p_n=0.02, p_gap=0.02)
+    t = build_tables(a, b, pi)
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).to(gpu)
+    ll1 = hmm.forward_loglik_device(model, plan, d_obs).cpu().numpy()
+    p1 = hmm.viterbi_device(model, plan, d_obs).cpu().numpy()
+    ll2, p2 = hmm.forward_viterbi_device(model, plan, d_obs)
+    ll2, p2 = ll2.cpu().numpy(), p2.cpu().numpy()
+    np.testing.assert_allclose(ll2, ll1, rtol=1e-12, atol=0)
+    np.testing.assert_array_equal(p2, p1)
+    np.testing.assert_array_equal(p2, O.viterbi(t, obs, off))
+    np.testing.assert_allclose(ll2, O.forward_loglik(t, obs, off), rtol=RTOL, atol=0)
