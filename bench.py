@@ -433,6 +433,7 @@ def main():
         if timing:
             fwd_ms.append(hmm.last_kernel_ms("forward"))
         if not xchg:
+            m1.close()
             return 0.0
         exchange()
         acc = 0.0
@@ -727,6 +728,11 @@ def main():
             **({"build_ms": round(float(np.mean(build_ms)), 1)} if opt_mode else {}),
             **({"per_rank_step_ms": per_rank_ms, "allreduce_ms": xchg_ms,
                 "allreduce_bytes": int(d_ll_global.numel() * 8)} if world > 1 else {}),
+            # optimize mode with a split build: each rank's own step still contains the
+            # build's all_gather, so it waits for the slowest rank's share of the build
+            **({"per_rank_includes": "model build incl. its all_gather (split_build)"}
+               if world > 1 and opt_mode and args.backend == "nccl" and args.split_build == 1
+               else {}),
             **({"host_path": host} if host is not None else {}),
             **({"shard_projection": shards} if shards is not None else {}),
             **(check or {}),

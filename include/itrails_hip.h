@@ -93,6 +93,12 @@ ITR_API int itr_plan_create(const int64_t* h_block_off, int64_t n_blocks, itr_pl
 ITR_API int itr_plan_create_ex(const int64_t* h_block_off, int64_t n_blocks, double split_frac,
                                double post_split_frac, itr_plan_t* out);
 ITR_API int itr_plan_destroy(itr_plan_t plan);
+/* The plan's work placement on a device with `cus` compute units, host-side only (no device
+ * needed): out[0..7] = forward+Viterbi long set (blocks, columns), its reserved CUs, the
+ * forward's reserved CUs, per-wave layout on (1/0), the Viterbi-only call's long set, the
+ * forward's VALU tasks, the mixed queue's entries.  For tests and diagnostics. */
+ITR_API int itr_plan_partition_info(const int64_t* h_block_off, int64_t n_blocks, int cus,
+                                    int64_t* out);
 ITR_API int itr_plan_total_columns(itr_plan_t plan, int64_t* total);
 /* grow the workspace now (optional; the sweeps grow it on demand) */
 ITR_API int itr_plan_reserve(itr_plan_t plan, int n_states, int for_posterior);

@@ -111,8 +111,9 @@ struct Partition {
   hipEvent_t fork = nullptr, jl = nullptr, jl2 = nullptr, jb = nullptr;
   std::vector<uint32_t> mb;    // the other CUs' mask
 };
-// The calling thread's partitions; destroyed with the thread (each thread that decodes owns
-// its streams, so a worker thread's exit returns its hardware-queue streams)
+// The calling thread's partitions, at most one per device; destroyed with the thread (each
+// thread that decodes owns its streams, so a worker thread's exit returns its hardware-queue
+// streams)
 struct Partitions {
   std::deque<Partition> v;
   static void destroy(Partition& x) {  // waits for the streams' work
@@ -145,10 +146,15 @@ int partition(int reserve, int reserve2, Partition** out, bool masked = true) {
       *out = &x;
       return 0;
     }
-  // one partition per thread: its three streams plus the caller's are the process's 4
-  // hardware queues (GPU_MAX_HW_QUEUES); a second partition's streams would share queues with
-  // the first's and serialise behind them
-  g_parts.release();
+  // one partition per thread and device: its three streams plus the caller's are the 4
+  // hardware queues the process gets on that device (GPU_MAX_HW_QUEUES); a second partition's
+  // streams would share queues with the first's and serialise behind them.  Only this
+  // device's partition is replaced (its work drained first); other devices' stay, so one
+  // thread can drive several GPUs in turn without re-creating streams.
+  Partition* slot = nullptr;
+  for (auto& x : g_parts.v)
+    if (x.device == dev) slot = &x;
+  if (slot) Partitions::destroy(*slot);
   const int cus = cu_count();
   const int nw = (cus + 31) / 32;
   std::vector<uint32_t> ml(nw, 0u), ml2(nw, 0u), mb(nw, 0u);
@@ -211,8 +217,13 @@ int partition(int reserve, int reserve2, Partition** out, bool masked = true) {
   HIP_TRY(hipEventCreateWithFlags(&x.jl2, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&x.jb, hipEventDisableTiming));
   x.mb = mb;
-  g_parts.v.push_back(x);
-  *out = &g_parts.v.back();
+  if (slot) {
+    *slot = x;  // (in place: the other devices' entries keep their addresses)
+  } else {
+    g_parts.v.push_back(x);
+    slot = &g_parts.v.back();
+  }
+  *out = slot;
   return 0;
 }
 
@@ -257,7 +268,6 @@ struct itr_plan {
   int64_t ntiles = 0;            // Viterbi tile records: sum over blocks of ceil(T / 16)
   int64_t* d_off = nullptr;
   int64_t* d_tile_off = nullptr;  // [nblocks+1] first tile record of every block
-  int* d_cubusy = nullptr;        // [4096] per-CU long-block counts (Viterbi hybrid)
   // posterior split (launch_post_split): the first npsplit blocks of the order get their
   // backward sweep concurrently with the forward one; beta rows at d_boff[block]
   int64_t npsplit = 0, beta_rows = 0;
@@ -349,8 +359,15 @@ int vit_stride(int n) {
 //               load (two waves per SIMD: ~640 ns alone), calibrated on the chr10 Viterbi-only
 //               call with 0 / 30 / 59 / 80 / 100 / 124 long blocks: 12.1 / 6.42 / 5.76 / 5.80 /
 //               6.02 / 7.97 ms (profiles/r4m_vit_long_set.txt; this rule picks 69)
+//   kMixFwd / kMixVit  the mixed queue's ordering weights: per-column step times under full
+//               load at N = 70 of a matrix-core forward group (~0.92 us) and a per-wave Viterbi
+//               block (~0.64 us), measured on chr10 (profiles/r3l_*)
+//   kMixPrio    mixed-queue entries that run at raised wave priority: about one per SIMD pair
+// Calibrated at N = 70 only; tests/test_partition.py pins the decisions they produce for the
+// benchmark layouts, so that a recalibration cannot move a layout onto another branch unseen.
 constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kBulkCu = 180e-9, kFwdValu = 370e-9,
-                 kBulkVit = 115e-9, kVitWaveLatV = 700e-9;
+                 kBulkVit = 115e-9, kVitWaveLatV = 700e-9, kMixFwd = 0.92, kMixVit = 0.64;
+constexpr int64_t kMixPrio = 512;
 
 // Bins of capacity `cap` (first fit, items longest first): the CUs a set of sequential tasks
 // needs to finish within cap
@@ -746,8 +763,11 @@ int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
   return itr_plan_create_ex(off, nblocks, -1.0, -1.0, out);
 }
 
-int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
-                       double post_split_frac, itr_plan_t* out) {
+namespace {
+// cus > 0: plan for that many CUs instead of the device's; host_only: the host-side plan
+// (task lists, CU partition) without device allocations or uploads (itr_plan_partition_info)
+int plan_create_impl(const int64_t* off, int64_t nblocks, double split_frac,
+                     double post_split_frac, int cus, bool host_only, itr_plan_t* out) {
   if (!out) return fail(ITR_EINVAL, "null output pointer");
   *out = nullptr;
   if (nblocks < 0 || (nblocks > 0 && !off)) return fail(ITR_EINVAL, "bad block offsets");
@@ -942,10 +962,9 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
     }
   }
   // Viterbi long set and the CU partition of the forward+Viterbi call
-  plan_partition(p, ulen, cu_count());
+  plan_partition(p, ulen, cus > 0 ? cus : cu_count());
   // The mixed queue: forward groups (steps = their longest member) and the remaining Viterbi
-  // blocks merged by expected duration, longest first.  Measured per-column step times under
-  // full load at N = 70: a forward group ~0.92 us, a per-wave Viterbi block ~0.64 us.
+  // blocks merged by expected duration (kMixFwd, kMixVit), longest first.
   std::vector<int32_t> mix;
   {
     const int64_t ng = (int64_t)groups_ll.size() / 4;
@@ -961,9 +980,9 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
     std::vector<int64_t> gidx(ng);
     std::iota(gidx.begin(), gidx.end(), 0);
     std::stable_sort(gidx.begin(), gidx.end(), [&](int64_t x, int64_t y) { return gsteps[x] > gsteps[y]; });
-    const double cf = 0.92, cv = 0.64;
+    const double cf = kMixFwd, cv = kMixVit;
     int64_t gi = 0, vi = p->vit_nlong;
-    const int64_t nprio = 512;  // about one per SIMD pair of the GPU
+    const int64_t nprio = kMixPrio;
     while (gi < ng || vi < nblocks) {
       const bool take_f = vi >= nblocks ||
                           (gi < ng && cf * (double)gsteps[gidx[gi]] >= cv * (double)p->sorted_len[vi]);
@@ -982,6 +1001,10 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
   p->nhsplit = (int64_t)hsplit_blk.size();
   p->ntasks = (int64_t)tasks.size() / 3;
   p->nsplit = (int64_t)split_blk.size();
+  if (host_only) {
+    *out = p;
+    return 0;
+  }
   int e = 0;
   if (!e) e = dev_alloc(&p->d_tasks, tasks.size());
   if (!e) e = dev_alloc(&p->d_wgroups, wgroups.size());
@@ -997,9 +1020,6 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
   if (!e) e = dev_alloc(&p->d_off, nblocks + 1);
   if (!e) e = dev_alloc(&p->d_tile_off, nblocks + 1);
   if (!e) e = dev_alloc(&p->d_boff, nblocks);
-  if (!e) e = dev_alloc(&p->d_cubusy, 4096);
-  if (!e && hipMemset(p->d_cubusy, 0, 4096 * sizeof(int)) != hipSuccess)
-    e = fail(ITR_EHIP, "plan workspace init failed");
   if (!e) e = dev_alloc(&p->d_order, nblocks);
   if (!e) e = dev_alloc(&p->d_queue, 16);
   if (!e && hipMemset(p->d_queue, 0, 16 * sizeof(int)) != hipSuccess)
@@ -1030,12 +1050,33 @@ int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
   *out = p;
   return 0;
 }
+}  // namespace
+
+int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
+                       double post_split_frac, itr_plan_t* out) {
+  return plan_create_impl(off, nblocks, split_frac, post_split_frac, 0, false, out);
+}
+
+int itr_plan_partition_info(const int64_t* off, int64_t nblocks, int cus, int64_t* out) {
+  if (!out || cus < 1) return fail(ITR_EINVAL, "bad arguments");
+  itr_plan_t p = nullptr;
+  if (int e = plan_create_impl(off, nblocks, -1.0, -1.0, cus, true, &p)) return e;
+  out[0] = p->vit_nlong;
+  out[1] = p->vit_long_cols;
+  out[2] = p->vit_reserve;
+  out[3] = p->fwd_reserve;
+  out[4] = p->wave_ok ? 1 : 0;
+  out[5] = p->vit_nlong_v;
+  out[6] = p->nutasks;
+  out[7] = p->nmix;
+  delete p;  // (host-only: nothing on the device)
+  return 0;
+}
 
 int itr_plan_destroy(itr_plan_t p) {
   if (!p) return 0;
   dev_free(p->d_off);
   dev_free(p->d_tile_off);
-  dev_free(p->d_cubusy);
   dev_free(p->d_boff);
   dev_free(p->d_beta);
   dev_free(p->d_order);

@@ -38,8 +38,6 @@ struct SweepArgs {
   double* beta;                 // MODE_BWD, optional: store the backward rows beta_t here
                                 //   (row beta_off[block] + t, stride XR) instead of posteriors
   const int64_t* beta_off;      //   [nblocks] first beta row of every split block
-  int* cu_busy;                 // MODE_VIT, optional: [4096] per-CU counts of exclusive blocks
-  int excl_len;                 //   blocks at least this long run alone on their CU
   const int32_t* tasks;         // MODE_FWD_LL: [nblocks x 3] {block, split, slot}, see capi.cpp
   double* svec;                 // MODE_FWD_LL: [nsplit x 2 x XR] vectors of split blocks
   int* sK;                      // MODE_FWD_LL: [nsplit x 2] their power-of-two exponents

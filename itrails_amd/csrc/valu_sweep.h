@@ -852,42 +852,18 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
   DIAG_FLUSH();
 }
 
-// Key of the CU this wave runs on (XCC, shader engine, shader array, CU; 256 distinct keys
-// on MI355X, scripts/micro/cu_key.hip).  Placement information for speed only.
-__device__ __forceinline__ int cu_key() {
-  const unsigned hw = __builtin_amdgcn_s_getreg(0xF804);   // HW_REG_HW_ID
-  const unsigned xcc = __builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
-  return ((((int)(xcc & 7) * 8 + (int)((hw >> 13) & 7)) * 2 + (int)((hw >> 12) & 1)) * 16 +
-          (int)((hw >> 8) & 0xF));
-}
-
 // The VALU-only persistent sweep: every workgroup pulls tasks longest first.
 template <int QL, int WV, int RJN, int IQ, int MODE>
 __device__ __forceinline__ void sweep_device(const SweepArgs& p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int qslot;
-  const int key = p.cu_busy ? cu_key() : 0;
   for (;;) {
-    if (threadIdx.x == 0) {
-      // while a long block is decoded alone on this CU, its co-resident workgroup sleeps
-      // at its next task boundary instead of competing for the CU's issue slots
-      if (p.cu_busy)
-        while (__hip_atomic_load(p.cu_busy + key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0)
-          __builtin_amdgcn_s_sleep(32);
-      qslot = atomicAdd(p.queue, 1);
-    }
+    if (threadIdx.x == 0) qslot = atomicAdd(p.queue, 1);
     lds_barrier();
     const int bi = uni(qslot);
     lds_barrier();
     if (bi >= p.nblocks) break;
-    bool excl = false;
-    if (p.cu_busy) {
-      const int blk = p.order[bi];
-      excl = p.off[blk + 1] - p.off[blk] >= p.excl_len;
-      if (excl && threadIdx.x == 0) atomicAdd(p.cu_busy + key, 1);
-    }
     sweep_task<QL, WV, RJN, IQ, MODE>(p, smem, bi);
-    if (excl && threadIdx.x == 0) atomicSub(p.cu_busy + key, 1);
   }
 }
 
