@@ -136,6 +136,21 @@ ITR_API int itr_forward_viterbi(itr_model_t model, itr_plan_t plan, const uint16
 ITR_API int itr_posterior(itr_model_t model, itr_plan_t plan, const uint16_t* d_obs,
                           double* d_post, void* stream);
 
+/* The reference's standalone sweep matrices of ONE block of T >= 1 columns, device pointers,
+ * float64 row-major, on `stream`:
+ *   kind 0  forward:  log alpha [T][N]                            (optimizer.py:165-188)
+ *   kind 1  backward: log beta [T][N], the reference's (w * e) @ a (optimizer.py:191-213)
+ *   kind 2  viterbi:  omega [T][N], and when d_prev is non-null the back-pointers
+ *           [T-1][N] as float64 state indices (first maximum)    (optimizer.py:305-333)
+ * omega and prev are exact; log alpha / log beta agree with the reference to rounding (its
+ * matrix-vector sums go through numpy's BLAS).  API-sized: one workgroup per call. */
+ITR_API int itr_block_rows(itr_model_t model, int kind, const uint16_t* d_obs, int64_t T,
+                           double* d_rows, double* d_prev, void* stream);
+/* backtrack_viterbi (optimizer.py:336-354): the path (float64 [T]) from omega [T][N] and
+ * prev [T-1][N] (device pointers, on `stream`). */
+ITR_API int itr_backtrack_rows(const double* d_omega, const double* d_prev, int64_t T, int n,
+                               double* d_path, void* stream);
+
 /* Packs the caller's per-block symbol arrays (the reference's V_lst: one int64 array per
  * MAF block, read_data.py:94-117, consumed by optimizer.py:40-116, 241-262, 357-377) into
  * the uint16 column array and int64 block offsets the sweeps take.  h_blocks[k] points at
@@ -237,6 +252,19 @@ ITR_API int itr_solve_batched(int n, int nrhs, int64_t batch, double* d_M, doubl
 ITR_API int itr_gemm_batched(int m, int n, int k, int64_t batch, double alpha,
                              const double* d_A, const double* d_B, double beta, double* d_C,
                              void* stream);
+
+/* One interval's chain-step products (run_markov_chain_ABC.py:13-33, 407-490): for group g
+ * (0 <= g < n_groups) and row r < rmax, entry e = g * rmax + r (d_src[e] < 0: padding):
+ *   d_out[d_dst[e]][:] = ((d_P[d_src[e]][cols] * d_F[d_oms[e]]) @ M_g) * d_F[d_ome[e]]
+ * with M_g = d_M + g * k * k (k x k row-major), cols = d_cols (k column indices of P; NULL:
+ * 0 .. k-1), d_oms / d_ome NULL for no mask.  Rows of d_P, d_F and d_out have strides ldp,
+ * ldf, ldo.  One fused MFMA pass (gather, mask, product, mask, scatter); d_out must not alias
+ * d_P.  Also the closing phase's per-task contractions (run_markov_chain_ABC.py:512-796). */
+ITR_API int itr_chain_rows(int k, int n_groups, int rmax, const int32_t* d_src,
+                           const int32_t* d_oms, const int32_t* d_ome, const int32_t* d_dst,
+                           const int32_t* d_cols, const double* d_P, int64_t ldp,
+                           const double* d_F, int64_t ldf, const double* d_M, double* d_out,
+                           int64_t ldo, void* stream);
 
 /* ---------------------------------------------------------------------------------- */
 /* model build: emission rows                                                          */

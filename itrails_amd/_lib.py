@@ -43,6 +43,8 @@ _SIGNATURES = {
     "itr_viterbi": ([_P, _P, _P, _P, _P], _I),
     "itr_forward_viterbi": ([_P, _P, _P, _P, _P, _P], _I),
     "itr_posterior": ([_P, _P, _P, _P, _P], _I),
+    "itr_block_rows": ([_P, _I, _P, _I64, _P, _P, _P], _I),
+    "itr_backtrack_rows": ([_P, _P, _I64, _I, _P, _P], _I),
     "itr_pack_symbols": ([_P, _P, _I64, _P, _P], _I),
     "itr_forward_loglik_host": ([_P, _P, _P, _P], _I),
     "itr_viterbi_host": ([_P, _P, _P, _P], _I),
@@ -58,6 +60,8 @@ _SIGNATURES = {
     "itr_vanloan_job_norms": ([_I, _P, _I, _P, _I, _P, _I64, _P, _P, _P, _P], _I),
     "itr_solve_batched": ([_I, _I, _I64, _P, _P, _P], _I),
     "itr_gemm_batched": ([_I, _I, _I, _I64, _D, _P, _P, _D, _P, _P], _I),
+    "itr_chain_rows": ([_I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _P, _I64, _P, _P, _I64, _P],
+                       _I),
     "itr_emission_rows": ([_I, _P, _P, _P], _I),
     "itr_maf_open": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_char_p,
                       ctypes.POINTER(_P)], _I),

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstring>
 #include <deque>
+#include <mutex>
 #include <numeric>
 #include <optional>
 #include <atomic>
@@ -247,10 +248,16 @@ struct itr_model {
   int n = 0;
   double *a = nullptr, *la = nullptr, *E = nullptr, *LE = nullptr, *PIE = nullptr,
          *LPIE = nullptr, *aT = nullptr;
-  // log E with rows padded to the one-block-per-wave Viterbi layout's width (-inf columns),
-  // when that layout serves this state count (wave_vit.hip)
+  // the one-block-per-wave Viterbi (wave_tasks.h), when that layout serves this state count
+  // (xrw = its slot count): log E in slot order padded to xrw columns (-inf), the state of
+  // every slot, max_{i != j} log a_ij per slot; built on the model's first Viterbi call
+  // (vit_slot_tables) from host copies of the tables kept until then
   double* LEW = nullptr;
+  int32_t* VSLOT = nullptr;
+  double* VMB = nullptr;
   int xrw = 0;
+  std::vector<double> h_a, h_la, h_LE, h_E, h_PIE;  // (E, PIE: the 256 N-free symbols)
+  std::mutex vit_mu;  // (the first Viterbi calls of several threads)
   // E padded to the per-wave matrix-core forward's width (zero columns) plus a row of ones
   // (row 625), when that layout serves this state count (wave_tasks.h)
   double* EF = nullptr;
@@ -659,20 +666,13 @@ int itr_model_create(int n, const double* a, const double* la, const double* E,
     return e;
   }
   const itr::WaveVitGeometry wv = itr::wave_vit_geometry(n);
-  if (wv.iq > 0) {
-    const int w = wv.xr;
-    std::vector<double> lew((size_t)ITR_NOBS * w, -INFINITY);
-    for (int o = 0; o < ITR_NOBS; ++o)
-      for (int j = 0; j < n; ++j) lew[(size_t)o * w + j] = LE[(size_t)o * n + j];
-    e = dev_alloc(&m->LEW, lew.size());
-    if (!e && hipMemcpy(m->LEW, lew.data(), lew.size() * sizeof(double),
-                        hipMemcpyHostToDevice) != hipSuccess)
-      e = fail(ITR_EHIP, "table upload failed");
-    if (e) {
-      itr_model_destroy(m);
-      return e;
-    }
-    m->xrw = w;
+  if (wv.iq > 0) {  // (the per-wave Viterbi's tables: on the first Viterbi call)
+    m->xrw = wv.xr;
+    m->h_a.assign(a, a + nn);
+    m->h_la.assign(la, la + nn);
+    m->h_LE.assign(LE, LE + on);
+    m->h_E.assign(E, E + (size_t)256 * n);
+    m->h_PIE.assign(PIE, PIE + (size_t)256 * n);
   }
   const itr::WaveMfmaGeometry wf = itr::wave_mfma_geometry(n);
 #ifdef ITR_EXPERIMENT
@@ -744,6 +744,8 @@ int itr_model_destroy(itr_model_t m) {
   dev_free(m->LPIE);
   dev_free(m->aT);
   dev_free(m->LEW);
+  dev_free(m->VSLOT);
+  dev_free(m->VMB);
   dev_free(m->EF);
   dev_free(m->LAT);
   dev_free(m->LDG);
@@ -900,7 +902,16 @@ int plan_create_impl(const int64_t* off, int64_t nblocks, double split_frac,
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_URGENT_FRAC")) ufrac = atof(getenv("ITR_URGENT_FRAC"));
 #endif
-  const double L = std::max(256.0, ufrac * (double)tmax);
+  double L = std::max(256.0, ufrac * (double)tmax);
+#ifdef ITR_EXPERIMENT
+  // makespan-based threshold: a matrix-core group stepping at ITR_URGENT_COLNS ns per column
+  // must finish its longest member within the plan's expected makespan
+  if (getenv("ITR_URGENT_COLNS")) {
+    const int ncu = cus > 0 ? cus : cu_count();
+    const double Tm = std::max((double)h_off[nblocks] * kBulkCu / ncu, (double)tmax * kVitLone);
+    L = std::max(256.0, Tm / (atof(getenv("ITR_URGENT_COLNS")) * 1e-9));
+  }
+#endif
   std::vector<int32_t> hsplit_blk, utasks, mtasks;
   std::vector<int64_t> ulen;
   struct MT { int32_t id; int64_t steps; bool bwd; };
@@ -1189,6 +1200,102 @@ int forward_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* logli
   return 0;
 }
 
+// The per-wave Viterbi's slot order (wave_tasks.h): a target column r of the layout is
+// scanned when any of its 8 target slots fails the bound test, so the states that fail
+// most often share the first columns.  How often a state fails is measured once per model
+// on the host: the bound test along 2,048 columns drawn from the model itself (8 blocks of
+// 256, hidden path from pi and a, N-free symbols from E), a few ms at N = 70.  The order only
+// moves work between scan columns; the decoded path does not depend on it.
+int vit_slot_tables(itr_model_t m) {
+  std::lock_guard<std::mutex> lock(m->vit_mu);
+  if (m->LEW) return 0;
+  const int n = m->n, w = m->xrw;
+  const std::vector<double>& la = m->h_la;
+  std::vector<double> mj(n, -INFINITY);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j)
+      if (i != j) mj[j] = std::max(mj[j], la[(size_t)i * n + j]);
+  std::vector<int> rank(n);
+  std::iota(rank.begin(), rank.end(), 0);
+#ifdef ITR_VIT_PRUNED
+  std::vector<int64_t> fails(n, 0);
+  uint64_t rs = 0x2545F4914F6CDD1Dull;
+  auto rnd = [&]() {  // splitmix64 -> [0, 1)
+    uint64_t z = (rs += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return (double)((z ^ (z >> 31)) >> 11) * 0x1.0p-53;
+  };
+  auto draw = [&](auto&& prob, int cnt) {  // index by cumulative weight
+    double tot = 0.0;
+    for (int k = 0; k < cnt; ++k) tot += prob(k);
+    double u = rnd() * tot;
+    for (int k = 0; k < cnt; ++k) {
+      u -= prob(k);
+      if (u < 0.0) return k;
+    }
+    return cnt - 1;
+  };
+  std::vector<double> om(n), nx(n);
+  for (int b = 0; b < 8; ++b) {
+    int s = draw([&](int j) { double v = 0.0; for (int o = 0; o < 256; ++o) v += m->h_PIE[(size_t)o * n + j]; return v; }, n);
+    int o = draw([&](int k) { return m->h_E[(size_t)k * n + s]; }, 256);
+    for (int j = 0; j < n; ++j) om[j] = std::log(m->h_PIE[(size_t)o * n + j]);
+    for (int t = 1; t < 256; ++t) {
+      s = draw([&](int j) { return m->h_a[(size_t)s * n + j]; }, n);
+      o = draw([&](int k) { return m->h_E[(size_t)k * n + s]; }, 256);
+      const double* le = m->h_LE.data() + (size_t)o * n;
+      const double top = *std::max_element(om.begin(), om.end());
+      for (int j = 0; j < n; ++j) {
+        const double yd = (om[j] + la[(size_t)j * n + j]) + le[j];
+        if (!(yd > (top + mj[j]) + le[j])) ++fails[j];
+        double yo = -INFINITY;
+        for (int i = 0; i < n; ++i)
+          if (i != j) yo = std::max(yo, om[i] + la[(size_t)i * n + j]);
+        nx[j] = std::max(yd, yo + le[j]);
+      }
+      om.swap(nx);
+    }
+  }
+  std::stable_sort(rank.begin(), rank.end(), [&](int x, int y) { return fails[x] > fails[y]; });
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_VSLOT_NATURAL")) std::iota(rank.begin(), rank.end(), 0);
+#endif
+  // rank k < 64: column k / 8 of group k % 8 (A slots); then the groups' B slots (column 8)
+  const int iq = w / 8;
+  std::vector<int32_t> slot(w, -1);
+  for (int k = 0; k < n; ++k)
+    slot[k < 8 * (iq - 1) ? iq * (k % 8) + k / 8 : iq * (k - 8 * (iq - 1)) + iq - 1] = rank[k];
+#else
+  std::vector<int32_t> slot(w, -1);  // the full-scan step: slot = state
+  for (int sl = 0; sl < n; ++sl) slot[sl] = rank[sl];
+#endif
+  std::vector<double> lew((size_t)ITR_NOBS * w, -INFINITY), vmb(w, -INFINITY);
+  for (int sl = 0; sl < w; ++sl) {
+    if (slot[sl] < 0) continue;
+    vmb[sl] = mj[slot[sl]];
+    for (int o = 0; o < ITR_NOBS; ++o) lew[(size_t)o * w + sl] = m->h_LE[(size_t)o * n + slot[sl]];
+  }
+  int e = dev_alloc(&m->VSLOT, (size_t)w);
+  if (!e) e = dev_alloc(&m->VMB, (size_t)w);
+  if (!e) e = dev_alloc(&m->LEW, lew.size());
+  if (!e && (hipMemcpy(m->VSLOT, slot.data(), w * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
+             hipMemcpy(m->VMB, vmb.data(), w * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+             hipMemcpy(m->LEW, lew.data(), lew.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess))
+    e = fail(ITR_EHIP, "table upload failed");
+  if (e) {
+    dev_free(m->VSLOT);
+    dev_free(m->VMB);
+    dev_free(m->LEW);
+    m->VSLOT = nullptr;
+    m->VMB = nullptr;
+    m->LEW = nullptr;
+    return e;
+  }
+  for (auto* v : {&m->h_a, &m->h_la, &m->h_LE, &m->h_E, &m->h_PIE}) std::vector<double>().swap(*v);
+  return 0;
+}
+
 itr::TraceArgs trace_args(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path) {
   itr::TraceArgs ta{};
   ta.n = m->n;
@@ -1321,9 +1428,11 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   };
   int64_t traced = 0;
   const itr::WaveVitGeometry wv = itr::wave_vit_geometry(m->n);
-  bool wave = wv.iq > 0 && m->LEW && m->xrw == wv.xr;
+  bool wave = wv.iq > 0 && m->xrw == wv.xr;
   const int cus = cu_count();
   if (wave && !p->wave_ok) wave = false;  // the long work would need more than half the CUs
+  if (wave)
+    if (int e = vit_slot_tables(m)) return e;
   // the reserved CU sets (plan_partition: sized for the forward+Viterbi call; the
   // Viterbi-only call runs on the same CU-masked streams, with its own long set swept by
   // both sets)
@@ -1381,6 +1490,8 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     w.la = m->la;
     w.lew = m->LEW;
     w.lpie = m->LPIE;
+    w.slot_state = m->VSLOT;
+    w.slot_m = m->VMB;
     w.ckpt = p->d_alpha;
     w.stay = p->d_stay;
     w.last_state = p->d_last;
@@ -1553,6 +1664,37 @@ int itr_forward_viterbi(itr_model_t m, itr_plan_t p, const uint16_t* obs, double
   if (!obs || !path || !loglik) return fail(ITR_EINVAL, "null device pointer");
   if (p->total == 0) return itr_forward_loglik(m, p, obs, loglik, stream);
   return viterbi_impl(m, p, obs, path, (hipStream_t)stream, loglik);
+}
+
+int itr_block_rows(itr_model_t m, int kind, const uint16_t* obs, int64_t T, double* rows,
+                   double* prev, void* stream) {
+  if (int e = check_model(m)) return e;
+  if (kind < 0 || kind > 2) return fail(ITR_EINVAL, "kind %d is not 0, 1 or 2", kind);
+  if (T < 1) return fail(ITR_EINVAL, "a block of %lld columns (the reference indexes V[0])",
+                         (long long)T);
+  if (!obs || !rows) return fail(ITR_EINVAL, "null device pointer");
+  itr::RowArgs a{};
+  a.kind = kind;
+  a.n = m->n;
+  a.T = T;
+  a.obs = obs;
+  a.a = m->a;
+  a.log_a = m->la;
+  a.emit = m->E;
+  a.log_emit = m->LE;
+  a.lpie = m->LPIE;
+  a.rows = rows;
+  a.prev = kind == 2 ? prev : nullptr;
+  HIP_TRY(itr::launch_rows(a, (hipStream_t)stream));
+  return 0;
+}
+
+int itr_backtrack_rows(const double* omega, const double* prev, int64_t T, int n, double* path,
+                       void* stream) {
+  if (T < 1 || n < 1 || n > ITR_MAX_STATES) return fail(ITR_EINVAL, "bad T / n");
+  if (!omega || !path || (T > 1 && !prev)) return fail(ITR_EINVAL, "null device pointer");
+  HIP_TRY(itr::launch_backtrack_rows(omega, prev, T, n, path, (hipStream_t)stream));
+  return 0;
 }
 
 int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post,
@@ -1896,6 +2038,21 @@ int itr_solve_batched(int n, int nrhs, int64_t batch, double* M, double* R, void
   const hipError_t e = itr::solve_batched(n, nrhs, batch, M, R, piv, st);
   (void)hipFreeAsync(piv, st);
   if (e != hipSuccess) return fail(ITR_EHIP, "solve failed: %s", hipGetErrorString(e));
+  return 0;
+}
+
+int itr_chain_rows(int k, int ng, int rmax, const int32_t* src, const int32_t* oms,
+                   const int32_t* ome, const int32_t* dst, const int32_t* cols, const double* P,
+                   int64_t ldp, const double* F, int64_t ldf, const double* M, double* out,
+                   int64_t ldo, void* stream) {
+  if (k < 1 || ng < 0 || rmax < 0 || ng > 65535)
+    return fail(ITR_EINVAL, "bad chain-rows shape k=%d groups=%d rmax=%d", k, ng, rmax);
+  if (ng == 0 || rmax == 0) return 0;
+  if (!src || !dst || !P || !M || !out || ((oms || ome) && !F))
+    return fail(ITR_EINVAL, "null device pointer");
+  itr::ChainRowsArgs a{k, rmax, src, oms, ome, dst, cols, P, ldp, F, ldf, M, out, ldo};
+  const hipError_t e = itr::chain_rows(a, ng, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ITR_EHIP, "chain rows failed: %s", hipGetErrorString(e));
   return 0;
 }
 

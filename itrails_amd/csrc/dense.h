@@ -23,6 +23,23 @@ struct GemmArgs {
 
 hipError_t gemm_batched(const GemmArgs& g, int64_t batch, hipStream_t st);
 
+// Chain-step rows (chain_rows_kernel): for the rows r < rmax of group g (entry e = g rmax + r,
+// src[e] < 0: padding), out[dst[e]] = ((P[src[e]][cols] * F[oms[e]]) @ M[g]) * F[ome[e]]
+// with M[g] k x k at M + g k k; cols (k entries) gathers P's columns (null: 0 .. k-1), oms /
+// ome select rows of F (null: no mask).
+struct ChainRowsArgs {
+  int k, rmax;
+  const int32_t *src, *oms, *ome, *dst, *cols;
+  const double* P;
+  int64_t ldp;
+  const double* F;
+  int64_t ldf;
+  const double* M;
+  double* out;
+  int64_t ldo;
+};
+hipError_t chain_rows(const ChainRowsArgs& a, int ngroups, hipStream_t st);
+
 // Solve M X = R for every member (M n x n, R n x nrhs, both row-major, contiguous):
 // M is overwritten by its LU factors (partial pivoting), R by X.  `piv` is a device
 // workspace of batch * n ints.

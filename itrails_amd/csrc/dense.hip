@@ -153,6 +153,103 @@ hipError_t gemm_batched(const GemmArgs& g, int64_t batch, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Chain-step rows (run_markov_chain_ABC.py:13-33 products, :407-490 per interval): the
+// gathered, masked row block of a group times the group's propagator, masked and scattered
+// in one pass — gemm_kernel's 64 x 64 tile and MFMA loop with the gathers in the A-tile
+// fetch and the mask and scatter in the epilogue (no V / result temporaries in HBM).
+__global__ void __launch_bounds__(256) chain_rows_kernel(ChainRowsArgs g) {
+  __shared__ double As[GBK][GBM + 2];
+  __shared__ double Bs[GBK][GBN + 2];
+  const int K = g.k;
+  const int tiles_n = (K + GBN - 1) / GBN;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  const int64_t e0 = (int64_t)blockIdx.y * g.rmax;
+  const double* __restrict__ B = g.M + (int64_t)blockIdx.y * K * K;
+  const int row0 = tm * GBM, col0 = tn * GBN;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+
+  dbl4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+  const int ar = tid >> 2, ak = (tid & 3) * 4;   // A tile: row ar, k ak..ak+3
+  const int bk = tid >> 4, bc = (tid & 15) * 4;  // B tile: k bk, cols bc..bc+3
+  const int arow = row0 + ar;
+  const int asrc = arow < g.rmax ? g.src[e0 + arow] : -1;
+  const double* prow = asrc >= 0 ? g.P + (int64_t)asrc * g.ldp : nullptr;
+  const double* frow = (asrc >= 0 && g.oms) ? g.F + (int64_t)g.oms[e0 + arow] * g.ldf : nullptr;
+  double ra[4], rb[4];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int gk = k0 + ak + e;
+      double v = 0.0;
+      if (prow && gk < K) {
+        v = prow[g.cols ? g.cols[gk] : gk];
+        if (frow) v *= frow[gk];
+      }
+      ra[e] = v;
+    }
+    const int gk = k0 + bk;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int gc = col0 + bc + e;
+      rb[e] = (gk < K && gc < K) ? B[(int64_t)gk * K + gc] : 0.0;
+    }
+  };
+  fetch(0);
+  for (int k0 = 0; k0 < K; k0 += GBK) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      As[ak + e][ar] = ra[e];
+      Bs[bk][bc + e] = rb[e];
+    }
+    __syncthreads();
+    if (k0 + GBK < K) fetch(k0 + GBK);
+#pragma unroll
+    for (int kk = 0; kk < GBK; kk += 4) {
+      double a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = As[kk + (l >> 4)][wr * 32 + i * 16 + (l & 15)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = Bs[kk + (l >> 4)][wc * 32 + j * 16 + (l & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + wr * 32 + i * 16 + (l >> 4) + 4 * r;
+      if (row >= g.rmax) continue;
+      const int64_t e = e0 + row;
+      if (g.src[e] < 0) continue;
+      double* orow = g.out + (int64_t)g.dst[e] * g.ldo;
+      const double* mrow = g.ome ? g.F + (int64_t)g.ome[e] * g.ldf : nullptr;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = col0 + wc * 32 + j * 16 + (l & 15);
+        if (col < K) orow[col] = mrow ? acc[i][j][r] * mrow[col] : acc[i][j][r];
+      }
+    }
+}
+
+hipError_t chain_rows(const ChainRowsArgs& a, int ngroups, hipStream_t st) {
+  if (ngroups <= 0 || a.rmax <= 0 || a.k <= 0) return hipSuccess;
+  if (ngroups > 65535) return hipErrorInvalidValue;
+  const int tiles = ((a.rmax + GBM - 1) / GBM) * ((a.k + GBN - 1) / GBN);
+  hipLaunchKernelGGL(chain_rows_kernel, dim3(tiles, (unsigned)ngroups), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 static hipError_t gemm(int m, int n, int k, Mat A, Mat B, Mat C, double alpha, Mat D,
                        double beta, double gamma, const int* idx, int64_t batch,
                        hipStream_t st) {

@@ -125,8 +125,10 @@ struct VitArgs {
   const int64_t* tile_off;      // [plan blocks + 1]
   const uint16_t* obs;          // [total]
   const double* la;             // log a, n x n
-  const double* lew;            // log E, 625 x xr (columns >= n: -inf)
+  const double* lew;            // log E, 625 x xr, columns in slot order (padding: -inf)
   const double* lpie;           // log(pi E), 625 x n
+  const int32_t* slot_state;    // [xr] state of each slot (-1: padding), wave_tasks.h
+  const double* slot_m;         // [xr] max_{i != j} log a_ij of the slot's state j
   double* ckpt;                 // [tiles x xr]
   uint16_t* stay;               // [tiles x xr]
   uint8_t* last_state;          // [plan blocks]
@@ -143,6 +145,20 @@ WaveVitGeometry wave_vit_geometry(int n);
 // role: 0 = bulk launch, 1 / 2 = a reserved set's late launch (only the kernel name differs)
 hipError_t launch_wave_vit(const WaveVitGeometry& g, int grid, const VitArgs& p,
                            hipStream_t st, int role = 0);
+
+// The reference's per-column matrices of one block (rows.hip): kind 0 = log alpha, 1 = log
+// beta, 2 = omega (+ prev when non-null); rows / prev are [T][n] / [T-1][n] float64
+struct RowArgs {
+  int kind, n;
+  int64_t T;
+  const uint16_t* obs;
+  const double *a, *log_a, *emit, *log_emit, *lpie;
+  double* rows;
+  double* prev;
+};
+hipError_t launch_rows(const RowArgs& p, hipStream_t st);
+hipError_t launch_backtrack_rows(const double* omega, const double* prev, int64_t T, int n,
+                                 double* path, hipStream_t st);
 
 // Viterbi by prediction and verification (pv_viterbi.hip): one block per wavefront, the
 // workgroup's waves sharing log a in LDS; same outputs as MODE_VIT

@@ -13,6 +13,16 @@
 namespace itr {
 namespace {
 
+#ifdef ITR_VIT_PRUNED
+template <int IQ>
+using VitLayout = WaveVit<IQ>;
+#define ITR_VIT_TASK vit_wave_task
+#else
+template <int IQ>
+using VitLayout = WaveVitFull<IQ>;
+#define ITR_VIT_TASK vit_wave_task_full
+#endif
+
 constexpr int kWaves = 4;  // independent wavefronts per workgroup
 
 // every lane takes part in the queue atomic (lane 0 adds 1): with a lane-divergent
@@ -27,11 +37,11 @@ __device__ __forceinline__ int next_task(int* queue) {
 template <int IQ, int ROLE>
 __global__ void __launch_bounds__(64 * kWaves, 2) wave_vit_kernel(VitArgs p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* wl = reinterpret_cast<double*>(smem) + (size_t)(threadIdx.x >> 6) * WaveVit<IQ>::WL;
+  double* wl = reinterpret_cast<double*>(smem) + (size_t)(threadIdx.x >> 6) * VitLayout<IQ>::WL;
   for (;;) {
     const int bi = next_task(p.queue);
     if (bi >= p.nblocks) break;
-    vit_wave_task<IQ>(p, wl, uni(p.order[bi]));
+    ITR_VIT_TASK<IQ>(p, wl, uni(p.order[bi]));
   }
 }
 
@@ -51,7 +61,7 @@ __global__ void __launch_bounds__(64 * kWaves, 2) wave_fwd_kernel(WaveMfmaArgs p
 // One queue of both kinds: entry e >= 0 = the Viterbi block e, e < 0 = forward group -e - 1.
 template <int IQ, int NT, int NK>
 struct Mixed {
-  static constexpr int WL = WaveVit<IQ>::WL > WF<NT, NK>::WL ? WaveVit<IQ>::WL : WF<NT, NK>::WL;
+  static constexpr int WL = VitLayout<IQ>::WL > WF<NT, NK>::WL ? VitLayout<IQ>::WL : WF<NT, NK>::WL;
 };
 template <int IQ, int NT, int NK, int ROLE>
 __global__ void __launch_bounds__(64 * kWaves, 2)
@@ -66,7 +76,7 @@ __global__ void __launch_bounds__(64 * kWaves, 2)
     if (e < 0) {
       fwd_wave_task<NT, NK>(f, wl, -e - 1);
     } else {
-      vit_wave_task<IQ>(v, wl, e);
+      ITR_VIT_TASK<IQ>(v, wl, e);
     }
   }
 }
@@ -99,7 +109,7 @@ WaveVitGeometry wave_vit_geometry(int n) {
   if (g.iq < 0) return g;
   g.block = 64 * kWaves;
   g.xr = 8 * g.iq;
-  g.lds = (size_t)kWaves * WaveVit<9>::WL * sizeof(double);
+  g.lds = (size_t)kWaves * VitLayout<9>::WL * sizeof(double);
   g.per_cu = occupancy(wave_vit_kernel<9, 0>, g.lds);
   return g;
 }

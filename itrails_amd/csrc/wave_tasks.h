@@ -6,33 +6,34 @@
 //
 // ---- Viterbi, one block per wavefront ----------------------------------------------------
 //
-// The 8-lanes-per-target layout of valu_sweep.h spends ~315 VALU instructions per column on
-// the (5,5) model (N = 70): every lane ends with the full maximum of its target after a
-// three-stage DPP all-reduce and runs the per-column tail redundantly, against 153 useful
-// adds/maxes.  Here one wavefront decodes a whole block on its own (no workgroup barrier):
+// One wavefront decodes a whole block on its own (no workgroup barrier; a wave's LDS
+// instructions execute in order).  The states are laid out in 8 IQ slots (IQ = 9: 72 slots
+// for N = 65..72), slot s = IQ g + r holding the state VSLOT[s] (the model's slot order,
+// capi.cpp vit_slot_tables).  Lane l = 8 g + q holds, in VGPRs, log a between the source
+// slots of chunk q (IQ q .. IQ q + IQ - 1) and the target slots of group g, and owns target
+// slot IQ g + q (A) and, for q = 0, target slot IQ g + IQ - 1 (B).
 //
-//   lane l = 8 q + g holds sources i in [IQ q, IQ q + IQ) x targets j in [IQ g, IQ g + IQ)
-//   of log a in VGPRs (loaded once per wave), forms the IQ partial maxima
-//   z_j = max_i (omega_i + log a_ij) over its sources (IQ^2 adds, IQ^2 - IQ maxes), writes
-//   them to the wave's partial table P[j][q] in LDS, and then finalises ONE target j = l
-//   (plus, for 8 IQ > 64, target 64 + (l & 7)) from the 8 partials of that target.
-//
-// ~181 VALU instructions per column at IQ = 9 (N <= 72).  All LDS traffic stays inside the
-// wave (a wave's LDS instructions execute in order), so a step needs no barrier.  The
-// emission rows are staged 8 columns at a time into the wave's LDS ring by direct-to-LDS
-// loads from a log-emission table padded to 8 IQ columns.
-//
-// Two such waves share a SIMD (256 VGPRs each), so a block steps at ~640 ns per column
-// (~1.7x the throughput of the 8-lane layout on short blocks, but ~2x its lone-step latency):
-// itr_viterbi gives the longest blocks to the 9-wave VALU layout on a reserved set of CUs and
-// this kernel the rest (capi.cpp); blocks at least p.prio_len long run at
-// raised wave priority.
+// Bound-pruned step (exact).  With Omega = max_i omega_i (a wave-wide maximum) and
+// M_j = max_{i != j} log a_ij (per model), rounding is monotone, so for every i != j
+//   fl(fl(omega_i + log a_ij) + log e_j) <= fl(fl(Omega + M_j) + log e_j) =: B_j.
+// A target whose stay score yd = fl(fl(omega_j + log a_jj) + log e_j) exceeds B_j has
+// yd > yo = max_{i != j} fl(fl(omega_i + log a_ij) + log e_j): its stay flag is 1 and
+// omega_t[j] = yd, bit for bit what the full scan gives.  Only the targets that fail the
+// test need the scan over all sources: for each target column r in which any group has a
+// failing target (a wave-uniform test on the ballot), the 8 lanes of every group form
+// max_k(omega + log a) over their source chunk for target IQ g + r and combine it by three
+// DPP steps; the owner takes its value.  On the (5,5) model, the bench workload (N = 70),
+// 84 % of the (column, target) pairs pass and 43 % of the columns need no scan at all;
+// with the slots ordered by how often a state fails (most often: column r = 0), a column
+// scans 2.2 target columns on average instead of 9.
 //
 // Outputs are those of the VALU sweep — the omega row of every 16-column tile's first column,
-// 16-bit stay-flag words, the last column's first argmax — from the identical arithmetic:
-// omega_t[j] = max(yd, yo), yd = (omega_j + log a_jj) + log e_j,
-// yo = max_{i != j}(omega_i + log a_ij) + log e_j (the max is exact and order-free), so the
-// traceback (hmm_sweeps.hip) is shared and paths are bit-identical.
+// 16-bit stay-flag words, the last column's first argmax (by state index) — so the
+// traceback (hmm_sweeps.hip) is shared and paths are bit-identical.  The emission rows
+// (slot order, padded to 8 IQ) are staged 8 columns at a time into the wave's LDS ring by
+// direct-to-LDS loads.  Two waves share a SIMD; itr_viterbi gives the longest blocks to the
+// 9-wave VALU layout on a reserved set of CUs and this kernel the rest (capi.cpp, DESIGN.md
+// §3.4); blocks at least p.prio_len long run at raised wave priority.
 //
 // ---- forward log-likelihood, four tasks per wavefront on the matrix cores ----------------
 //
@@ -81,21 +82,20 @@ __device__ __forceinline__ int lane_id_fresh() {
 
 template <int IQ>
 struct WaveVit {
-  static constexpr int XRW = 8 * IQ;                  // targets = sources of the layout
-  static constexpr int NB = XRW > 64 ? XRW - 64 : 0;  // second targets: 64 + (l & 7)
-  static_assert(NB <= 8, "at most 8 second targets");
+  static_assert(IQ == 9, "8 A slots and one B slot per target group");
+  static constexpr int XRW = 8 * IQ;                  // slots
   static constexpr int IQS = IQ + (IQ & 1);           // 16-byte aligned source chunks
   static constexpr int XN = 8 * IQS;                  // published vector slots
-  static constexpr int PS = 10;  // partial row stride: 8 chunks + 2 (conflict-free b128 reads)
   static constexpr int HT = 8;   // columns per staged emission half-tile
   // a half-tile of emission rows [HT][XRW] arrives by NI direct-to-LDS loads of 16 bytes per
   // lane (1 KiB each); the buffer is rounded up to whole loads
   static constexpr int NI = (HT * XRW + 127) / 128, EB = 128 * NI;
   static_assert(XRW % 2 == 0, "16-byte pieces must not cross a row");
-  // per-wave LDS (doubles): published vector + 64 sink slots, partials, emission ring [2],
-  // symbol ring [2][64] (uint16)
-  static constexpr int LX = XN + 64, LP = XRW * PS, LE = 2 * EB, LS = 2 * 64 / 4;
-  static constexpr int WL = LX + LP + LE + LS;
+  // per-wave LDS (doubles): published vector + 64 sink slots, emission ring [2], symbol ring
+  // [2][64] (uint16), the lanes' log a of target column IQ - 1 [IQ][64] (out of VGPRs: that
+  // column, the B slots, is scanned least often)
+  static constexpr int LX = XN + 64, LE = 2 * EB, LS = 2 * 64 / 4, LM = IQ * 64;
+  static constexpr int WL = LX + LE + LS + LM;
 };
 
 // X row stride (doubles) with conflict-free ds_read_b128 A-operand reads: lane l reads row
@@ -155,9 +155,261 @@ __device__ __forceinline__ double row16_sum_w(double v) {
   return v + dpp_f64<0x128>(v);
 }
 
+// maximum over the wave, uniform (every lane's value counts)
+__device__ __forceinline__ double wave_max_u(double v) {
+  v = fmax(v, dpp_f64<DPP_Q1>(v));
+  v = fmax(v, dpp_f64<DPP_Q2>(v));
+  v = fmax(v, dpp_f64<DPP_HM>(v));
+  v = fmax(v, dpp_f64<DPP_R8>(v));
+  return rows4_max(v);
+}
+
 template <int IQ>
 __device__ __forceinline__ void vit_wave_task(const VitArgs& p, double* wl, int blk) {
   using C = WaveVit<IQ>;
+  constexpr int IQS = C::IQS, XN = C::XN, HT = C::HT, NI = C::NI, EB = C::EB, XRW = C::XRW;
+  const int l = lane_id_fresh(), g = l >> 3, q = l & 7;
+  const int n = p.n;
+  const int64_t xr = p.xr;
+  double* X = wl;
+  double* EST = X + C::LX;
+  uint16_t* SYM = reinterpret_cast<uint16_t*>(EST + C::LE);
+  double* M8 = EST + C::LE + C::LS;
+
+  // owned target slots and their states (-1: padding)
+  const int slA = IQ * g + q, slB = IQ * g + IQ - 1;
+  const int stA = p.slot_state[slA];
+  const int stB = q == 0 ? p.slot_state[slB] : -1;
+  const bool inA = stA >= 0, inB = stB >= 0;
+  // log a slice: source slots IQ q + k, target slots IQ g + r (r < IQ - 1 in VGPRs, r = IQ - 1
+  // in M8); the diagonal stays out
+  double m[IQ][IQ - 1];
+#pragma unroll
+  for (int k = 0; k < IQ; ++k) {
+    const int si = p.slot_state[IQ * q + k];
+#pragma unroll
+    for (int r = 0; r < IQ; ++r) {
+      const int sj = p.slot_state[IQ * g + r];
+      const double v = (si >= 0 && sj >= 0 && si != sj) ? p.la[(int64_t)si * n + sj] : -INFINITY;
+      if (r < IQ - 1)
+        m[k][r] = v;
+      else
+        M8[k * 64 + l] = v;
+    }
+  }
+  const double ldA = inA ? p.la[(int64_t)stA * n + stA] : -INFINITY;
+  const double ldB = inB ? p.la[(int64_t)stB * n + stB] : -INFINITY;
+  const double mA = inA ? p.slot_m[slA] : -INFINITY;
+  const double mB = inB ? p.slot_m[slB] : -INFINITY;
+  const int xiA = g * IQS + q;                          // X positions (B of q > 0: a sink)
+  const int xiB = q == 0 ? g * IQS + IQ - 1 : XN + l;
+  for (int i = l; i < C::LX; i += 64) X[i] = -INFINITY;
+
+  const int64_t c0 = uni64(p.off[blk]);
+  const int T = uni((int)(p.off[blk + 1] - c0));
+  if (T > 0) {  // (no `continue` in this loop, same reason)
+    const bool urgent = T >= p.prio_len;
+    if (urgent) __builtin_amdgcn_s_setprio(3);
+    const uint16_t* ob = p.obs + c0;
+    // raw symbol loads; the clamp into the alphabet (memory safety only) is applied when a
+    // chunk is committed to SYM, 64 columns after its load was issued (a clamp right at
+    // the load would make the wave wait for it there)
+    auto symg = [&](int s) -> int { return (int)ob[min(s, T - 1)]; };
+    auto clamp_sym = [](int v) -> uint16_t { return (uint16_t)min(v, 624); };
+    // symbols: chunks of 64 columns, two resident in SYM, the next one in flight
+    SYM[l] = clamp_sym(symg(l));
+    SYM[64 + l] = clamp_sym(symg(64 + l));
+    int sin = symg(128 + l);
+    auto sym = [&](int s) -> int { return SYM[((s >> 6) & 1) * 64 + (s & 63)]; };
+    // emission rows of half-tile h -> EST[h & 1] (row-major [HT][XRW]) by direct-to-LDS
+    // loads; the compiler does not track them, so every read of a half-tile follows an
+    // explicit vmcnt(0) (stage_wait) a half-tile after its loads were issued
+    auto stage_issue = [&](int h) {
+      double* d = EST + (h & 1) * EB;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int e = 128 * i + 2 * l;
+        const double* src = p.lew;
+        if (e < HT * XRW) src += (int64_t)sym(h * HT + e / XRW) * XRW + e % XRW;
+        __builtin_amdgcn_global_load_lds(
+            src, (__attribute__((address_space(3))) void*)(d + 128 * i), 16, 0, 0);
+      }
+    };
+    auto stage_wait = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+    const int o0 = sym(0);
+    double xA = inA ? p.lpie[o0 * n + stA] : -INFINITY;
+    double xB = inB ? p.lpie[o0 * n + stB] : -INFINITY;
+    X[xiA] = xA;
+    X[xiB] = xB;
+    const int64_t tk0 = uni64(p.tile_off[blk]);
+    // this block's checkpoint rows and flag words (tiles x xr records from tile tk0, by
+    // state), stored through buffer resources: lane part = the state, uniform part = the
+    // tile's record; a lane without a state stores out of bounds (nothing)
+    const uint32_t nrec = (uint32_t)((T + VIT_TILE - 1) / VIT_TILE * xr);
+    const __amdgpu_buffer_rsrc_t rck = buf_rsrc(p.ckpt + tk0 * xr, nrec * 8);
+    const __amdgpu_buffer_rsrc_t rst = buf_rsrc(p.stay + tk0 * xr, nrec * 2);
+    const uint32_t vA = inA ? (uint32_t)stA : kOffNone / 8, vB = inB ? (uint32_t)stB : kOffNone / 8;
+    buf_store_f64(rck, vA * 8, 0, xA);
+    buf_store_f64(rck, vB * 8, 0, xB);
+    stage_issue(0);
+    stage_wait();
+    stage_issue(1);
+    wave_lds_sync();
+    // Stores are issued between a staging wait and the next staging issue: the checkpoint
+    // row of a tile's first column at the following half-tile boundary, a tile's flag
+    // words at the next tile's first boundary (or after the block).  A store issued just
+    // before a vmcnt(0) would be waited for there.
+    uint32_t pbA = 0, pbB = 0;
+    int prec = -1;        // flag record of the previous tile (relative to tk0 * xr)
+    int ckrec = -1;       // pending checkpoint row (record), its values
+    double ckA = 0.0, ckB = 0.0;
+    for (int t0 = 0; t0 < T; t0 += VIT_TILE) {
+      const int rec = (t0 / VIT_TILE) * (int)xr;
+      uint32_t bA = 0, bB = 0;
+#ifdef ITR_VIT_UNROLL_TILE
+#pragma unroll
+#else
+      // (not unrolled: sixteen copies of the step with its scan columns would fill the
+      // instruction cache the CU shares with its neighbour)
+#pragma unroll 1
+#endif
+      for (int sub = 0; sub < VIT_TILE; ++sub) {
+        const int t = t0 + sub;
+        if (t >= 1 && t < T) {
+          if ((sub & (HT - 1)) == 0) {  // half-tile boundary (t >= 8)
+            stage_wait();
+            if (ckrec >= 0) {
+              buf_store_f64(rck, vA * 8, (uint32_t)ckrec * 8, ckA);
+              buf_store_f64(rck, vB * 8, (uint32_t)ckrec * 8, ckB);
+              ckrec = -1;
+            }
+            if (sub == 0 && prec >= 0) {  // the previous tile's flag words
+              buf_store_u16(rst, vA * 2, (uint32_t)prec * 2, (uint16_t)pbA);
+              buf_store_u16(rst, vB * 2, (uint32_t)prec * 2, (uint16_t)pbB);
+              prec = -1;
+            }
+            if ((t & 63) == 0) {  // next symbol chunk in, the one after requested
+              SYM[(((t >> 6) + 1) & 1) * 64 + l] = clamp_sym(sin);
+              sin = symg(t + 128 + l);
+            }
+            stage_issue(t / HT + 1);
+          }
+          const double* es = EST + ((t / HT) & 1) * EB + (t & (HT - 1)) * XRW;
+          const double ecA = es[slA];
+          const double ecB = es[slB];
+          // omega_{t-1} of source chunk q (the scans' operands; over a group's 8 lanes, every
+          // slot: Omega from them by a tree and three DPP steps, no cross-row traffic)
+          double xs[IQ];
+#pragma unroll
+          for (int k = 0; k < IQ; ++k) xs[k] = X[q * IQS + k];
+          double om = fmax(fmax(fmax(xs[0], xs[1]), fmax(xs[2], xs[3])),
+                           fmax(fmax(xs[4], xs[5]), fmax(xs[6], xs[7])));
+          if constexpr (IQ > 8) om = fmax(om, xs[8]);
+          om = fmax(om, dpp_f64<DPP_Q1>(om));
+          om = fmax(om, dpp_f64<DPP_Q2>(om));
+          om = fmax(om, dpp_f64<DPP_HM>(om));
+          const double ydA = (xA + ldA) + ecA;
+          const double ydB = (xB + ldB) + ecB;
+          // the bound test (exact: see the header)
+          const bool failA = inA && !(ydA > (om + mA) + ecA);
+          const bool failB = inB && !(ydB > (om + mB) + ecB);
+          const uint64_t fA = __builtin_amdgcn_ballot_w64(failA);
+          const uint64_t fB = __builtin_amdgcn_ballot_w64(failB);
+          double zA = -INFINITY, zB = -INFINITY;
+          // max over the group's lanes of the chunk maxima of target column r
+          auto scan = [&](int r) {
+            double y[IQ];
+#pragma unroll
+            for (int k = 0; k < IQ; ++k) y[k] = xs[k] + (r < IQ - 1 ? m[k][r] : M8[k * 64 + l]);
+            double z = fmax(fmax(fmax(y[0], y[1]), fmax(y[2], y[3])),
+                            fmax(fmax(y[4], y[5]), fmax(y[6], y[7])));
+            if constexpr (IQ > 8) z = fmax(z, y[8]);
+            return z;
+          };
+          auto group_max = [](double z) {
+            z = fmax(z, dpp_f64<DPP_Q1>(z));
+            z = fmax(z, dpp_f64<DPP_Q2>(z));
+            return fmax(z, dpp_f64<DPP_HM>(z));
+          };
+          if ((fA | fB) != 0) {
+            // target columns two at a time (two independent chains: the wave's step is
+            // latency-bound), a pair when either of its columns has a failing target
+#pragma unroll
+            for (int r = 0; r < IQ - 1; r += 2) {
+              if ((fA & (0x0303030303030303ull << r)) != 0) {
+                double z0 = scan(r), z1 = scan(r + 1);
+                z0 = group_max(z0);
+                z1 = group_max(z1);
+                zA = q == r ? z0 : (q == r + 1 ? z1 : zA);
+              }
+            }
+            if (fB != 0) zB = group_max(scan(IQ - 1));
+          }
+          const double yoA = zA + ecA;
+          const double yoB = zB + ecB;
+          bA |= (uint32_t)(ydA > yoA) << sub;
+          bB |= (uint32_t)(ydB > yoB) << sub;
+          xA = fmax(ydA, yoA);
+          xB = fmax(ydB, yoB);
+          X[xiA] = xA;
+          X[xiB] = xB;
+          wave_lds_sync();  // omega_t visible to every lane for the next step
+          if (sub == 0) {  // the tile's checkpoint row (t = t0 >= 16), stored later
+            ckrec = rec;
+            ckA = xA;
+            ckB = xB;
+          }
+        }
+      }
+      pbA = bA;
+      pbB = bB;
+      prec = rec;
+    }
+    if (ckrec >= 0) {  // a checkpoint row whose half-tile boundary was past the block
+      buf_store_f64(rck, vA * 8, (uint32_t)ckrec * 8, ckA);
+      buf_store_f64(rck, vB * 8, (uint32_t)ckrec * 8, ckB);
+    }
+    buf_store_u16(rst, vA * 2, (uint32_t)prec * 2, (uint16_t)pbA);  // the last tile's flags
+    buf_store_u16(rst, vB * 2, (uint32_t)prec * 2, (uint16_t)pbB);
+    // last state = first argmax of omega_{T-1} by state index (optimizer.py:346)
+    double bv = inA ? xA : -INFINITY;
+    int bj = inA ? stA : 0x7fffffff;
+    if (inB && (xB > bv || (xB == bv && stB < bj))) {
+      bv = xB;
+      bj = stB;
+    }
+    wave_first_max(bv, bj);
+    if (l == 0) p.last_state[blk] = (uint8_t)bj;
+    if (urgent) __builtin_amdgcn_s_setprio(0);
+  }
+}
+
+#ifndef ITR_VIT_PRUNED
+// The full-scan per-wave step (the product step until the bound-pruned one above, built with
+// -DITR_VIT_PRUNED, is faster): lane l = 8 q + g, partial table in LDS, slots = states
+// (capi.cpp builds the identity slot order for it).
+template <int IQ>
+struct WaveVitFull {
+  static constexpr int XRW = 8 * IQ;                  // targets = sources of the layout
+  static constexpr int NB = XRW > 64 ? XRW - 64 : 0;  // second targets: 64 + (l & 7)
+  static_assert(NB <= 8, "at most 8 second targets");
+  static constexpr int IQS = IQ + (IQ & 1);           // 16-byte aligned source chunks
+  static constexpr int XN = 8 * IQS;                  // published vector slots
+  static constexpr int PS = 10;  // partial row stride: 8 chunks + 2 (conflict-free b128 reads)
+  static constexpr int HT = 8;   // columns per staged emission half-tile
+  // a half-tile of emission rows [HT][XRW] arrives by NI direct-to-LDS loads of 16 bytes per
+  // lane (1 KiB each); the buffer is rounded up to whole loads
+  static constexpr int NI = (HT * XRW + 127) / 128, EB = 128 * NI;
+  static_assert(XRW % 2 == 0, "16-byte pieces must not cross a row");
+  // per-wave LDS (doubles): published vector + 64 sink slots, partials, emission ring [2],
+  // symbol ring [2][64] (uint16)
+  static constexpr int LX = XN + 64, LP = XRW * PS, LE = 2 * EB, LS = 2 * 64 / 4;
+  static constexpr int WL = LX + LP + LE + LS;
+};
+
+template <int IQ>
+__device__ __forceinline__ void vit_wave_task_full(const VitArgs& p, double* wl, int blk) {
+  using C = WaveVitFull<IQ>;
   constexpr int XRW = C::XRW, NB = C::NB, IQS = C::IQS, XN = C::XN, PS = C::PS, HT = C::HT,
                 NI = C::NI, EB = C::EB;
   // q high, g low: a 16-lane store group of the partial writes (ds_write_b64, banks mod 32)
@@ -340,6 +592,8 @@ __device__ __forceinline__ void vit_wave_task(const VitArgs& p, double* wl, int 
     if (urgent) __builtin_amdgcn_s_setprio(0);
   }
 }
+
+#endif
 
 template <int NT, int NK>
 __device__ __forceinline__ void fwd_wave_task(const WaveMfmaArgs& p, double* wl, int gi) {

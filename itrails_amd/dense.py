@@ -162,3 +162,16 @@ def gemm_batched(A, B, alpha=1.0):
                                      float(alpha), dA.data_ptr(), dB.data_ptr(), 0.0,
                                      C.data_ptr(), _stream()))
     return C if on_dev else C.cpu().numpy()
+
+
+def chain_rows(P, F, M, tab, out, cols=None):
+    """One interval's chain-step products on device (itr_chain_rows): for the entries of
+    `tab` = (src, oms, ome, dst, ngroups, rmax) (int32 device tensors [ngroups * rmax], -1
+    padding; oms / ome may be None), out[dst] = ((P[src][:, cols] * F[oms]) @ M[g]) * F[ome]."""
+    src, oms, ome, dst, ng, rmax = tab
+    k = M.shape[-1]
+    p = lambda x: x.data_ptr() if x is not None else None  # noqa: E731
+    check(lib().itr_chain_rows(k, ng, rmax, p(src), p(oms), p(ome), p(dst), p(cols), P.data_ptr(),
+                               P.shape[1], p(F), F.shape[1] if F is not None else 0,
+                               M.data_ptr(), out.data_ptr(), out.shape[1], _stream()))
+    return out

@@ -7,9 +7,10 @@ Two layers:
   every call is one C-ABI call (include/itrails_hip.h) on the current torch stream.
 * Reference layer — the functions of optimizer.py:145-377 with the same names, arguments,
   return types and semantics (`forward_loglik`, `loglik_wrapper`, `loglik_wrapper_par`,
-  `viterbi_wrapper`, `post_prob`, `post_prob_wrapper`, `backtrack`-free `viterbi`), so a
-  caller written against the reference drops in unchanged.  `order` arguments are accepted
-  and ignored: the alphabet expansion is tabulated once (itrails_amd/tables.py).
+  `viterbi_wrapper`, `post_prob`, `post_prob_wrapper`, and the standalone sweeps `forward`,
+  `backward`, `viterbi` (omega, prev) and `backtrack_viterbi`), so a caller written against
+  the reference drops in unchanged.  `order` arguments are accepted and ignored: the alphabet
+  expansion is tabulated once (itrails_amd/tables.py).
 
 No code path here computes on the host: if libitrails_hip.so is missing or the device is
 unavailable the calls raise.
@@ -28,7 +29,8 @@ from .tables import HmmTables, build_tables
 __all__ = [
     "Model", "Plan", "concat_blocks", "forward_loglik_device", "viterbi_device",
     "posterior_device", "forward_loglik", "loglik_wrapper", "loglik_wrapper_par",
-    "viterbi_wrapper", "post_prob", "post_prob_wrapper", "block_logliks",
+    "viterbi_wrapper", "post_prob", "post_prob_wrapper", "block_logliks", "forward",
+    "backward", "viterbi", "backtrack_viterbi", "block_rows_device",
 ]
 
 
@@ -210,6 +212,31 @@ def posterior_device(model: Model, plan: Plan, d_obs, out=None):
     return out
 
 
+ROWS_FORWARD, ROWS_BACKWARD, ROWS_VITERBI = 0, 1, 2
+
+
+def block_rows_device(model: Model, kind: int, d_obs, out=None, out_prev=None):
+    """The reference's matrices of ONE block (itr_block_rows): kind 0 log alpha, 1 log beta,
+    2 omega (and, with out_prev or kind 2 by default, the back-pointers [T-1, N]); float64
+    [T, N] on device.  Returns rows, or (omega, prev) for kind 2."""
+    import torch
+
+    if d_obs.dtype not in (torch.int16, torch.uint16) or not d_obs.is_cuda \
+            or not d_obs.is_contiguous():
+        raise TypeError("d_obs must be a contiguous int16/uint16 device tensor")
+    T = d_obs.numel()
+    if T < 1:
+        raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+    out = _out(out, (T, model.n), torch.float64, d_obs.device)
+    prev = None
+    if kind == ROWS_VITERBI:
+        prev = _out(out_prev, (T - 1, model.n), torch.float64, d_obs.device)
+    check(lib().itr_block_rows(model.handle, int(kind), ptr(d_obs), T, ptr(out),
+                               ptr(prev) if prev is not None and T > 1 else None,
+                               _stream_handle()))
+    return (out, prev) if kind == ROWS_VITERBI else out
+
+
 def last_kernel_ms(which: str) -> float:
     v = ctypes.c_double()
     check(lib().itr_last_kernel_ms(which.encode(), ctypes.byref(v)))
@@ -295,3 +322,56 @@ def post_prob_wrapper(a, b, pi, V_lst: Iterable[np.ndarray]) -> List[np.ndarray]
 def post_prob(a, b, pi, V, order=None) -> np.ndarray:
     """Posterior matrix of one block (optimizer.py:216-238)."""
     return post_prob_wrapper(a, b, pi, [V])[0]
+
+
+# the standalone sweeps (optimizer.py:165-213, 305-354): one block, numpy in and out
+def _one_block(V):
+    import torch
+
+    obs, _ = concat_blocks([np.asarray(V)])
+    if obs.size == 0:
+        raise IndexError("index 0 is out of bounds for axis 0 with size 0")
+    return torch.from_numpy(obs.astype(np.int16)).cuda()
+
+
+def forward(a, b, pi, V, order=None) -> np.ndarray:
+    """Log-scaled forward matrix alpha (T x N float64) of one block (optimizer.py:165-188)."""
+    d_obs = _one_block(V)
+    model = Model(a, b, pi)
+    return block_rows_device(model, ROWS_FORWARD, d_obs).cpu().numpy()
+
+
+def backward(a, b, V, order=None) -> np.ndarray:
+    """Log-scaled backward matrix beta (T x N float64) of one block, with the reference's
+    (beta * e) @ a recursion (optimizer.py:191-213)."""
+    d_obs = _one_block(V)
+    n = np.asarray(a).shape[0]
+    model = Model(a, b, np.full(n, 1.0 / n))  # (pi takes no part in beta)
+    return block_rows_device(model, ROWS_BACKWARD, d_obs).cpu().numpy()
+
+
+def viterbi(a, b, pi, V, order=None):
+    """(omega, prev) of one block (optimizer.py:305-333): omega T x N, prev (T-1) x N float64
+    back-pointers (first maximum, like np.argmax)."""
+    d_obs = _one_block(V)
+    model = Model(a, b, pi)
+    omega, prev = block_rows_device(model, ROWS_VITERBI, d_obs)
+    return omega.cpu().numpy(), prev.cpu().numpy()
+
+
+def backtrack_viterbi(omega, prev) -> np.ndarray:
+    """The Viterbi path (float64 [T]) from omega and prev (optimizer.py:336-354)."""
+    import torch
+
+    omega = np.ascontiguousarray(omega, dtype=np.float64)
+    T = omega.shape[0]
+    if T < 1:
+        raise IndexError("index -1 is out of bounds for axis 0 with size 0")
+    n = omega.shape[1]
+    prev = np.ascontiguousarray(prev, dtype=np.float64).reshape(max(T - 1, 0), n)
+    d_om = torch.from_numpy(omega).cuda()
+    d_prev = torch.from_numpy(prev).cuda() if T > 1 else None
+    d_path = torch.empty(T, dtype=torch.float64, device=d_om.device)
+    check(lib().itr_backtrack_rows(ptr(d_om), ptr(d_prev) if d_prev is not None else None, T, n,
+                                   ptr(d_path), _stream_handle()))
+    return d_path.cpu().numpy()

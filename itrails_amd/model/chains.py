@@ -536,16 +536,30 @@ def _device_tables(plan, Q, ss, la):
     off = np.zeros(len(job) + 1, dtype=np.int64)
     np.cumsum(lens, out=off[1:])
     T = lambda a: torch.as_tensor(np.asarray(a, dtype=np.int64), device=dev)  # noqa: E731
+    T32 = lambda a: torch.as_tensor(np.asarray(a, dtype=np.int32), device=dev)  # noqa: E731
+
+    def rows_table(ng, rmax, gid, slot, cols):
+        """itr_chain_rows entry tables: [ng * rmax] int32, -1 padding."""
+        out = []
+        for c in cols:
+            t = np.full(ng * rmax, -1, dtype=np.int32)
+            if c is not None:
+                t[np.asarray(gid) * rmax + np.asarray(slot)] = c
+            out.append(T32(t) if c is not None else None)
+        return (*out, ng, rmax)
+
     for d, ip in zip(ivs, plan.intervals):
         src, oms, ome, dst = ip.plain
-        d.plain = (T(src), T(oms), T(ome), T(dst)) if src.size else None
+        d.plain = rows_table(1, src.size, np.zeros(src.size, np.int64), np.arange(src.size),
+                             (src, oms, ome, dst)) if src.size else None
         d.ng = len(ip.groups)
         pids_list = [g[0] for g in ip.groups]
         d.sum_steps, (gid, slot), d.rmax = _group_tables(dev, pids_list,
                                                          [g[1].size for g in ip.groups])
         if d.ng:
             cat = lambda j: np.concatenate([g[j] for g in ip.groups])  # noqa: E731
-            d.rows = (T(cat(1)), T(cat(2)), T(cat(3)), T(cat(4)), gid, slot)
+            d.rows = rows_table(d.ng, d.rmax, gid.cpu().numpy(), slot.cpu().numpy(),
+                                (cat(1), cat(2), cat(3), cat(4)))
         else:
             d.rows = None
     tab = {
@@ -563,8 +577,11 @@ def _device_tables(plan, Q, ss, la):
     tab["c_steps"], (cg, cs), tab["c_rmax"] = _group_tables(
         dev, cpids, [g[2].size for g in plan.close_groups])
     if plan.close_groups:
-        tab["c_rows"] = (T(np.concatenate([g[2] for g in plan.close_groups])), cg, cs,
-                         T(np.concatenate([g[1] for g in plan.close_groups])))
+        rws = np.concatenate([g[2] for g in plan.close_groups])
+        tasks = np.concatenate([g[1] for g in plan.close_groups])
+        tab["c_rows"] = rows_table(len(plan.close_groups), tab["c_rmax"], cg.cpu().numpy(),
+                                   cs.cpu().numpy(), (rws, None, None, tasks))
+    tab["keep32"] = T32(np.nonzero(keep)[0])
     tab["ntasks"] = sum(len(t) for _, t, _ in plan.close_groups)
     plan.dev[key] = tab
     return tab
@@ -741,16 +758,15 @@ def _run_chain_abc_device(plan, Q, times, ss, probs: Dict, la) -> Dict:
     for i, v in enumerate(probs.values()):
         P0[i] = v[0]
     P[:len(probs)] = torch.from_numpy(P0).to(dev)
+    from ..dense import chain_rows
     for d, (E, M) in zip(tab["ivs"], EM):
+        # (P * mask) @ propagator * mask for every key row of the interval, gathered, multiplied
+        # and scattered by one fused kernel per matrix kind (itr_chain_rows)
         Pn = P.clone()
         if d.plain is not None:
-            src, oms, ome, dst = d.plain
-            Pn[dst] = ((P[src] * F[oms]) @ E) * F[ome]
+            chain_rows(P, F, E.contiguous(), d.plain, Pn)
         if d.rows is not None:
-            src, oms, ome, dst, gid, slot = d.rows
-            V = torch.zeros((d.ng, d.rmax, n), dtype=torch.float64, device=dev)
-            V[gid, slot] = P[src] * F[oms]
-            Pn[dst] = torch.bmm(V, M)[gid, slot] * F[ome]
+            chain_rows(P, F, M.contiguous(), d.rows, Pn)
         P = Pn
     absorbing = (7, 7)
     keep = tab["keep"]
@@ -760,13 +776,12 @@ def _run_chain_abc_device(plan, Q, times, ss, probs: Dict, la) -> Dict:
     deep = torch.zeros(tab["ntasks"], dtype=torch.float64, device=dev)
     if plan.close_paths:
         D = la.deepest_t(Qn, masks_without(masks, absorbing), plan.close_paths)
-        rws, gid, slot, tasks = tab["c_rows"]
         ng = len(plan.close_groups)
         nk = keep.numel()
         M = _group_matrices(D, tab["c_steps"], ng, nk)
-        V = torch.zeros((ng, tab["c_rmax"], nk), dtype=torch.float64, device=dev)
-        V[gid, slot] = P[rws][:, keep]
-        deep[tasks] = torch.bmm(V, M)[gid, slot].sum(dim=1)
+        R = torch.zeros((tab["ntasks"], nk), dtype=torch.float64, device=dev)
+        chain_rows(P, None, M.contiguous(), tab["c_rows"], R, cols=tab["keep32"])
+        deep = R.sum(dim=1)
     host = torch.cat([sums, deep]).cpu().numpy()
     ns = sums.numel()
     out: Dict = {}

@@ -234,3 +234,40 @@ def test_vanloan_paths_interval_branch_vs_per_path(gpu):
         ref = expm_blocktri_batched((C * t[0])[None], L)[0][:n, -n:]
         scale = max(np.abs(ref).max(), 1.0)
         assert np.abs(got[k] - ref).max() <= 1e-13 * scale, (k, np.abs(got[k] - ref).max())
+
+
+@pytest.mark.parametrize("k,ng,rmax", [(203, 3, 70), (15, 1, 5), (130, 2, 200)])
+def test_chain_rows_vs_numpy(gpu, k, ng, rmax):
+    """itr_chain_rows (the fused chain-step products of the device model build) against the
+    same gathers, masks and products in NumPy: every written row, padding rows untouched."""
+    import torch
+    from itrails_amd.dense import chain_rows
+
+    rng = np.random.default_rng(k + ng)
+    n = k + 7 if k == 130 else k  # (column gather: P wider than the matrices)
+    nrows = ng * rmax + 5
+    P = rng.random((nrows, n))
+    F = (rng.random((9, k)) < 0.7).astype(np.float64)
+    M = rng.random((ng, k, k)) / k
+    src = rng.integers(0, nrows, size=ng * rmax).astype(np.int32)
+    src[rng.random(src.size) < 0.2] = -1
+    oms = rng.integers(0, 9, size=src.size).astype(np.int32)
+    ome = rng.integers(0, 9, size=src.size).astype(np.int32)
+    dst = rng.permutation(nrows)[:src.size].astype(np.int32)
+    cols = np.sort(rng.choice(n, size=k, replace=False)).astype(np.int32) if n > k else None
+    d = lambda x: torch.from_numpy(x).to(gpu) if x is not None else None  # noqa: E731
+    out = torch.full((nrows, k), -1.0, dtype=torch.float64, device=gpu)
+    use_masks = cols is None
+    tab = (d(src), d(oms) if use_masks else None, d(ome) if use_masks else None, d(dst), ng, rmax)
+    chain_rows(d(P), d(F) if use_masks else None, d(M), tab, out, cols=d(cols))
+    got = out.cpu().numpy()
+    want = np.full((nrows, k), -1.0)
+    for e in range(src.size):
+        if src[e] < 0:
+            continue
+        v = P[src[e]][cols] if cols is not None else P[src[e]].copy()
+        if use_masks:
+            v = v * F[oms[e]]
+        r = v @ M[e // rmax]
+        want[dst[e]] = r * F[ome[e]] if use_masks else r
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-15)

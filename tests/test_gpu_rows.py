@@ -1,0 +1,77 @@
+"""The reference's standalone sweep functions on the device (hmm.forward, hmm.backward,
+hmm.viterbi, hmm.backtrack_viterbi -> itr_block_rows / itr_backtrack_rows, rows.hip) against
+the row-level oracle (oracle/rows_oracle.py) and the reference-generated goldens
+(tests/golden/sweep_*.npz), block by block, with the reference's shapes and dtypes.
+
+Bars: omega, prev and paths identical; log alpha / log beta to 1e-10 relative (sums in
+another order than numpy's BLAS); log-likelihoods and posteriors built from them to 1e-8.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+from itrails_amd import hmm
+from itrails_amd.tables import build_tables
+from oracle import rows_oracle as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["sweep_syn4.npz", "sweep_syn13.npz", "sweep_kat_3_3.npz",
+                                  "sweep_syn70.npz"])
+def test_rows_vs_oracle_and_goldens(gpu, name):
+    g = golden(name)
+    a, b, pi = g["a"], g["b"], g["pi"]
+    t = build_tables(a, b, pi)
+    obs, off = g["obs"].astype(np.int64), g["off"]
+    for k in range(len(off) - 1):
+        V = obs[off[k]:off[k + 1]]
+        if V.size == 0:
+            with pytest.raises(IndexError):
+                hmm.forward(a, b, pi, V)
+            continue
+        V = V[:1500]  # (the oracle loops in Python)
+        alpha = hmm.forward(a, b, pi, V)
+        beta = hmm.backward(a, b, V)
+        omega, prev = hmm.viterbi(a, b, pi, V)
+        path = hmm.backtrack_viterbi(omega, prev)
+        assert alpha.shape == beta.shape == omega.shape == (len(V), t.n)
+        assert prev.shape == (len(V) - 1, t.n) and prev.dtype == np.float64
+        assert path.dtype == np.float64 and path.shape == (len(V),)
+        np.testing.assert_allclose(alpha, R.forward(t, V), rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(beta, R.backward(t, V), rtol=1e-10, atol=1e-10)
+        om_ref, prev_ref = R.viterbi(t, V)
+        np.testing.assert_array_equal(omega, om_ref)
+        np.testing.assert_array_equal(prev, prev_ref)
+        np.testing.assert_array_equal(path, R.backtrack_viterbi(om_ref, prev_ref))
+        if len(V) == off[k + 1] - off[k]:  # whole block: the reference's own outputs
+            ll = R.loglik_from_alpha(alpha)
+            assert abs(ll - g["loglik"][k]) <= 1e-8 * abs(g["loglik"][k])
+            np.testing.assert_array_equal(path, g["path"][off[k]:off[k + 1]])
+            rows = g["post_rows"]
+            sel = (rows >= off[k]) & (rows < off[k + 1])
+            np.testing.assert_allclose(R.post_from_rows(alpha, beta)[rows[sel] - off[k]],
+                                       g["post"][sel], rtol=1e-8, atol=1e-300)
+
+
+def test_rows_single_column_and_ties(gpu):
+    """T = 1 (no back-pointers), and flat transitions with duplicated emissions (exact ties:
+    first maximum)."""
+    rng = np.random.default_rng(3)
+    n = 12
+    a = np.full((n, n), 1.0 / n)
+    b = np.repeat(rng.dirichlet(np.full(256, 0.5), size=n // 2), 2, axis=0)
+    pi = np.full(n, 1.0 / n)
+    t = build_tables(a, b, pi)
+    V1 = np.array([17])
+    omega, prev = hmm.viterbi(a, b, pi, V1)
+    assert prev.shape == (0, n)
+    np.testing.assert_array_equal(omega, R.viterbi(t, V1)[0])
+    np.testing.assert_array_equal(hmm.backtrack_viterbi(omega, prev),
+                                  [float(np.argmax(omega[0]))])
+    V = rng.integers(0, 625, size=400)
+    omega, prev = hmm.viterbi(a, b, pi, V)
+    om_ref, prev_ref = R.viterbi(t, V)
+    np.testing.assert_array_equal(prev, prev_ref)
+    np.testing.assert_array_equal(hmm.backtrack_viterbi(omega, prev),
+                                  R.backtrack_viterbi(om_ref, prev_ref))

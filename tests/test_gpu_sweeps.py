@@ -84,6 +84,58 @@ def test_ties_first_maximum(gpu):
     np.testing.assert_array_equal(hmm._paths(model, plan, obs), O.viterbi(t, obs, off))
 
 
+@pytest.mark.parametrize("combined", [False, True])
+def test_bound_fails_everywhere(gpu, combined):
+    """Flat transitions and duplicated emission rows: the per-wave Viterbi's bound test
+    (wave_tasks.h) fails for every target of every column, so every column runs all nine
+    scan columns, and the exact ties must still resolve to the lowest state.  Hundreds of
+    blocks under 2,048 columns, so the per-wave layout takes them (itr_viterbi and
+    itr_forward_viterbi)."""
+    import torch
+
+    rng = np.random.default_rng(6)
+    n = 70
+    a = np.full((n, n), 1.0 / n)
+    b = np.repeat(rng.dirichlet(np.full(256, 0.5), size=n // 2), 2, axis=0)
+    pi = np.full(n, 1.0 / n)
+    lengths = [1, 2, 17, 2000] + list(rng.integers(1, 2000, size=300))
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=11)
+    t = build_tables(a, b, pi)
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).to(gpu)
+    if combined:
+        ll, path = hmm.forward_viterbi_device(model, plan, d_obs)
+        np.testing.assert_allclose(ll.cpu().numpy(), O.forward_loglik(t, obs, off), rtol=RTOL,
+                                   atol=0)
+    else:
+        path = hmm.viterbi_device(model, plan, d_obs)
+    np.testing.assert_array_equal(path.cpu().numpy(), O.viterbi(t, obs, off))
+
+
+@pytest.mark.parametrize("n", [65, 70, 72])
+def test_viterbi_zero_probabilities(gpu, n):
+    """Zeros in a, b and pi (log 0 = -inf in the Viterbi's sums): unreachable states,
+    impossible emissions and targets without any off-diagonal source, at the state counts of
+    the per-wave layout."""
+    rng = np.random.default_rng(90 + n)
+    a, b, pi = random_hmm(rng, n, stay=(0.5, 0.99))
+    a[rng.random((n, n)) < 0.5] = 0.0
+    a[:, 3] = 0.0
+    a[np.arange(n), np.arange(n)] = 0.5
+    a[3, :] = 0.0
+    a[3, 3] = 1.0  # state 3: no incoming transitions from other states
+    a /= a.sum(1, keepdims=True)
+    b[rng.random((n, 256)) < 0.3] = 0.0
+    b /= b.sum(1, keepdims=True)
+    pi[rng.random(n) < 0.3] = 0.0
+    pi /= pi.sum()
+    lengths = list(rng.integers(1, 1800, size=200)) + [1, 2, 3000]
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=n, p_n=0.02, p_gap=0.01)
+    t = build_tables(a, b, pi)
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    np.testing.assert_array_equal(hmm._paths(model, plan, obs), O.viterbi(t, obs, off))
+
+
 @pytest.mark.parametrize("name", [m for m in model_fixtures() if m != "model_kat_1_1.npz"]
                          + int_model_fixtures())
 def test_reference_models_vs_oracle(gpu, name):
