@@ -758,15 +758,14 @@ def _run_chain_abc_device(plan, Q, times, ss, probs: Dict, la) -> Dict:
     for i, v in enumerate(probs.values()):
         P0[i] = v[0]
     P[:len(probs)] = torch.from_numpy(P0).to(dev)
-    from ..dense import chain_rows
     for d, (E, M) in zip(tab["ivs"], EM):
         # (P * mask) @ propagator * mask for every key row of the interval, gathered, multiplied
         # and scattered by one fused kernel per matrix kind (itr_chain_rows)
         Pn = P.clone()
         if d.plain is not None:
-            chain_rows(P, F, E.contiguous(), d.plain, Pn)
+            la.chain_rows(P, F, E.contiguous(), d.plain, Pn)
         if d.rows is not None:
-            chain_rows(P, F, M.contiguous(), d.rows, Pn)
+            la.chain_rows(P, F, M.contiguous(), d.rows, Pn)
         P = Pn
     absorbing = (7, 7)
     keep = tab["keep"]
@@ -780,7 +779,7 @@ def _run_chain_abc_device(plan, Q, times, ss, probs: Dict, la) -> Dict:
         nk = keep.numel()
         M = _group_matrices(D, tab["c_steps"], ng, nk)
         R = torch.zeros((tab["ntasks"], nk), dtype=torch.float64, device=dev)
-        chain_rows(P, None, M.contiguous(), tab["c_rows"], R, cols=tab["keep32"])
+        la.chain_rows(P, None, M.contiguous(), tab["c_rows"], R, cols=tab["keep32"])
         deep = R.sum(dim=1)
     host = torch.cat([sums, deep]).cpu().numpy()
     ns = sums.numel()

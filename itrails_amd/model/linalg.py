@@ -198,6 +198,12 @@ class DeviceLinalg:
             return []
         return list(self.deepest_t(Q, masks, paths).cpu().numpy())
 
+    def chain_rows(self, P, F, M, tab, out, cols=None):
+        """One interval's chain-step products, gathered, masked and scattered in one fused
+        MFMA pass (dense.chain_rows, itr_chain_rows)."""
+        from ..dense import chain_rows
+        return chain_rows(P, F, M, tab, out, cols=cols)
+
     def rowmat(self, V: np.ndarray, M: np.ndarray) -> np.ndarray:
         """V @ M for a stack of row vectors V (k x n) and one n x n propagator: the per-key
         vector-matrix products of a chain interval as one MFMA GEMM (dense.hip)."""

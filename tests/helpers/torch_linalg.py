@@ -72,3 +72,22 @@ class FakeTorchLinalg(FakeNumpyLinalg):
         D = self.deepest(Q, masks, paths)
         return torch.from_numpy(np.stack(D)) if D else torch.zeros((0, n, n),
                                                                    dtype=torch.float64)
+
+    def chain_rows(self, P, F, M, tab, out, cols=None):
+        """The semantics of itr_chain_rows in torch (CPU)."""
+        src, oms, ome, dst, ng, rmax = tab
+        for e in range(ng * rmax):
+            s = int(src[e])
+            if s < 0:
+                continue
+            v = P[s][cols.long()] if cols is not None else P[s]
+            if oms is not None:
+                v = v * F[int(oms[e])]
+            # (np.einsum: one fixed summation order whatever the thread count, so the split
+            # build's ranks and the single-rank build round alike)
+            Mg = M[e // rmax] if M.dim() == 3 else M
+            r = torch.from_numpy(np.einsum("i,ij->j", v.numpy(), Mg.numpy()))
+            if ome is not None:
+                r = r * F[int(ome[e])]
+            out[int(dst[e])] = r
+        return out
