@@ -8,12 +8,12 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["hmm_sweeps.hip", "mfma_sweeps.hip", "wave_sweeps.hip", "pv_viterbi.hip", "dense.hip", "vanloan.hip", "emission.hip", "rows.hip", "maf.cpp", "writers.cpp", "capi.cpp"]
+SOURCES = ["hmm_sweeps.hip", "mfma_sweeps.hip", "wave_sweeps.hip", "dense.hip", "vanloan.hip", "emission.hip", "rows.hip", "maf.cpp", "writers.cpp", "capi.cpp"]
 OUT = os.path.join(HERE, "libitrails_hip.so")
 # The sweeps never produce NaN (log 0 = -inf is the only non-finite value, and no
 # inf - inf or 0/0 is formed), so fmax needs no NaN-quieting canonicalize after each DPP
 # move; infinities keep their IEEE semantics (no -ffinite-math-only).
-EXTRA = {"hmm_sweeps.hip": ["-fno-honor-nans"], "mfma_sweeps.hip": ["-fno-honor-nans"], "wave_sweeps.hip": ["-fno-honor-nans"], "pv_viterbi.hip": ["-fno-honor-nans"]}
+EXTRA = {"hmm_sweeps.hip": ["-fno-honor-nans"], "mfma_sweeps.hip": ["-fno-honor-nans"], "wave_sweeps.hip": ["-fno-honor-nans"]}
 ARCH = os.environ.get("ITR_OFFLOAD_ARCH", "gfx950")
 
 

@@ -262,11 +262,6 @@ struct itr_model {
   // (row 625), when that layout serves this state count (wave_tasks.h)
   double* EF = nullptr;
   int erf = 0;
-  // the prediction-and-verification Viterbi (pv_viterbi.hip): log a^T (rows padded to rsa
-  // with -inf), log a_jj, max_{i != j} log a_ij, and log E padded to xe columns (-inf), when
-  // that layout serves this state count
-  double *LAT = nullptr, *LDG = nullptr, *LMJ = nullptr, *LEP = nullptr;
-  bool pv_safe = true;  // some omega can be -inf: a zero in pi E or E, or an unreachable state
 };
 
 struct itr_plan {
@@ -285,7 +280,7 @@ struct itr_plan {
   int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep,
                            // [3, 4] hybrid sweeps, [5, 6] Viterbi hybrid, [7] per-wave Viterbi,
                            // [8, 9] the idle loop of a split hybrid launch, [10] per-wave forward,
-                           // [12] mixed launch, [13] the long blocks' traceback, [14] pv Viterbi
+                           // [12] mixed launch, [13] the long blocks' traceback
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
   std::vector<int64_t> sorted_len;  // block lengths, longest first (processing order)
@@ -696,40 +691,6 @@ int itr_model_create(int n, const double* a, const double* la, const double* E,
     }
     m->erf = w;
   }
-  const itr::PvGeometry pg = itr::pv_geometry(n);
-  if (pg.ns > 0) {
-    std::vector<double> lat((size_t)n * pg.rsa, -INFINITY), ldg(n), lmj(n, -INFINITY);
-    std::vector<double> lep((size_t)ITR_NOBS * pg.xe, -INFINITY);
-    for (int i = 0; i < n; ++i)
-      for (int j = 0; j < n; ++j) {
-        const double v = la[(size_t)i * n + j];
-        lat[(size_t)j * pg.rsa + i] = v;
-        if (i == j)
-          ldg[j] = v;
-        else
-          lmj[j] = std::max(lmj[j], v);
-      }
-    bool inf = false;
-    for (int o = 0; o < ITR_NOBS; ++o)
-      for (int j = 0; j < n; ++j) {
-        lep[(size_t)o * pg.xe + j] = LE[(size_t)o * n + j];
-        inf = inf || !(LE[(size_t)o * n + j] > -INFINITY) || !(LPIE[(size_t)o * n + j] > -INFINITY);
-      }
-    for (int j = 0; j < n && !inf; ++j) inf = !(lmj[j] > -INFINITY) && !(ldg[j] > -INFINITY);
-    m->pv_safe = inf;
-    double** dst2[4] = {&m->LAT, &m->LDG, &m->LMJ, &m->LEP};
-    const std::vector<double>* src2[4] = {&lat, &ldg, &lmj, &lep};
-    for (int i = 0; i < 4 && !e; ++i) {
-      e = dev_alloc(dst2[i], src2[i]->size());
-      if (!e && hipMemcpy(*dst2[i], src2[i]->data(), src2[i]->size() * sizeof(double),
-                          hipMemcpyHostToDevice) != hipSuccess)
-        e = fail(ITR_EHIP, "table upload failed");
-    }
-    if (e) {
-      itr_model_destroy(m);
-      return e;
-    }
-  }
   *out = m;
   return 0;
 }
@@ -747,10 +708,6 @@ int itr_model_destroy(itr_model_t m) {
   dev_free(m->VSLOT);
   dev_free(m->VMB);
   dev_free(m->EF);
-  dev_free(m->LAT);
-  dev_free(m->LDG);
-  dev_free(m->LMJ);
-  dev_free(m->LEP);
   delete m;
   return 0;
 }
@@ -1313,69 +1270,6 @@ itr::TraceArgs trace_args(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint
   return ta;
 }
 
-// The prediction-and-verification Viterbi (pv_viterbi.hip) serves every state count its LDS
-// layout fits (N <= 128)
-bool use_pv(itr_model_t m) {
-  const char* e = getenv("ITR_PV");  // (while the layout is being tuned: opt-in)
-  return m->LAT != nullptr && e && e[0] == '1';
-}
-
-// Viterbi by prediction and verification: one persistent launch over every block (longest
-// first, one wave per block, the longest ones spread one per CU), then the traceback; with
-// fwd_loglik the forward log-likelihood sweep first on the same stream.
-int pv_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path, hipStream_t st,
-            double* fwd_loglik) {
-  std::optional<Scope> both;  // the combined call's timer, traceback excluded
-  if (fwd_loglik) {
-    both.emplace("forward_viterbi", st);
-    if (int e = forward_impl(m, p, obs, fwd_loglik, st, 0)) return e;
-  }
-  const itr::PvGeometry g = itr::pv_geometry(m->n);
-  itr::PvArgs a{};
-  a.n = m->n;
-  a.xr = vit_stride(m->n);
-  a.nblocks = p->nblocks;
-  a.order = p->d_order;
-  a.queue = p->d_queue + 14;
-  a.off = p->d_off;
-  a.tile_off = p->d_tile_off;
-  a.obs = obs;
-  a.lat = m->LAT;
-  a.ldg = m->LDG;
-  a.lmj = m->LMJ;
-  a.lep = m->LEP;
-  a.lpie = m->LPIE;
-  a.ckpt = p->d_alpha;
-  a.stay = p->d_stay;
-  a.last_state = p->d_last;
-  a.safe = m->pv_safe ? 1 : 0;
-  const int cus = cu_count();
-  // the ~CU-count longest blocks at raised wave priority against the co-resident waves
-  a.prio_len = (int)std::max<int64_t>(
-      1, p->sorted_len[std::min<int64_t>(p->nblocks - 1, (int64_t)cus - 1)]);
-  const int grid = (int)std::min<int64_t>(cus, p->nblocks);
-  HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
-#ifdef ITR_DIAG
-  if (!g_diag) HIP_TRY(hipMalloc(&g_diag, 16 * sizeof(uint64_t)));
-  HIP_TRY(hipMemsetAsync(g_diag, 0, 16 * sizeof(uint64_t), st));
-  a.diag = g_diag;
-#endif
-  {
-    std::optional<Scope> sc;
-    if (!fwd_loglik) sc.emplace("viterbi", st);
-    HIP_TRY(itr::launch_pv_vit(g, grid, a, st));
-  }
-  both.reset();
-  itr::TraceArgs ta = trace_args(m, p, obs, path);
-  ta.nblocks = p->nblocks;
-  ta.order = p->d_order;
-  const int64_t tgrid = std::min<int64_t>((ta.nblocks + 3) / 4, (int64_t)cus * 4);
-  HIP_TRY(hipMemsetAsync(ta.queue, 0, sizeof(int), st));
-  Scope sc("traceback", st);
-  HIP_TRY(itr::launch_vit_traceback(ta, (int)tgrid, st));
-  return 0;
-}
-
 // The Viterbi sweep and traceback of every block into `path`; with fwd_loglik, the forward
 // log-likelihood sweep too, overlapped with the Viterbi sweep's longest blocks.
 //
@@ -1396,7 +1290,6 @@ int pv_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path, hip
 int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path,
                  hipStream_t st, double* fwd_loglik) {
   if (int e = reserve(p, m->n, true, false)) return e;
-  if (use_pv(m)) return pv_impl(m, p, obs, path, st, fwd_loglik);
   std::optional<Scope> both;  // the combined call's timer: fork to join, traceback excluded
   if (fwd_loglik) both.emplace("forward_viterbi", st);
   itr::SweepArgs a = base_args(m, p, obs);

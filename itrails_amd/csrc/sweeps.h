@@ -160,46 +160,6 @@ hipError_t launch_rows(const RowArgs& p, hipStream_t st);
 hipError_t launch_backtrack_rows(const double* omega, const double* prev, int64_t T, int n,
                                  double* path, hipStream_t st);
 
-// Viterbi by prediction and verification (pv_viterbi.hip): one block per wavefront, the
-// workgroup's waves sharing log a in LDS; same outputs as MODE_VIT
-struct PvArgs {
-  int n;                        // hidden states
-  int xr;                       // record stride of the checkpoint rows / flag words
-  int64_t nblocks;              // blocks of `order`
-  const int32_t* order;         // [nblocks] longest first
-  int* queue;                   // work counter, zero at launch
-  const int64_t* off;           // [plan blocks + 1]
-  const int64_t* tile_off;      // [plan blocks + 1]
-  const uint16_t* obs;          // [total]
-  const double* lat;            // log a^T with -inf padding: n x rsa
-  const double* ldg;            // [n] log a_jj
-  const double* lmj;            // [n] max_{i != j} log a_ij
-  const double* lep;            // log E padded to xe columns (-inf): 625 x xe
-  const double* lpie;           // log(pi E), 625 x n
-  double* ckpt;                 // [tiles x xr]
-  uint16_t* stay;               // [tiles x xr]
-  uint8_t* last_state;          // [plan blocks]
-  int prio_len;                 // blocks at least this long run at raised wave priority
-  int safe;                     // some omega can be -inf (model with zero probabilities)
-  uint64_t* diag;               // diagnostic build only: event counts and phase cycles
-  // layout (set by launch_pv_vit from the geometry)
-  int rsa, rs, rss, xe, eb, lcap, wl;
-};
-struct PvGeometry {
-  int ns;       // target slots per lane (negative: no such layout for this n)
-  int waves;    // wavefronts per workgroup (one workgroup per CU)
-  int block;    // threads per workgroup
-  int rsa;      // row stride of lat (= 2 mod 4)
-  int rs, rss;  // LDS value row width (multiple of 16) and stride
-  int xe;       // row width of lep (even >= n)
-  int eb;       // doubles of a wave's emission staging buffer
-  int lcap;     // scanned pairs per window at most
-  int wl;       // doubles of LDS per wave
-  size_t lds;   // dynamic LDS bytes per workgroup
-};
-PvGeometry pv_geometry(int n);
-hipError_t launch_pv_vit(const PvGeometry& g, int grid, PvArgs a, hipStream_t st);
-
 // The forward log-likelihood sweep with one group of four tasks per wavefront on the matrix
 // cores (wave_fwd.hip): the throughput form for short tasks
 struct WaveMfmaArgs {
