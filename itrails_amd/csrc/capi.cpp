@@ -365,10 +365,16 @@ int vit_stride(int n) {
 //               load at N = 70 of a matrix-core forward group (~0.92 us) and a per-wave Viterbi
 //               block (~0.64 us), measured on chr10 (profiles/r3l_*)
 //   kMixPrio    mixed-queue entries that run at raised wave priority: about one per SIMD pair
+//   kMixGroupCol  the per-column step a forward half may take in a matrix-core group and
+//               still finish within the expected makespan (sets the floor of the VALU-task
+//               threshold): chr100 world-8 shards with 0.7 / 1.0 / 1.4 us -> slowest shard
+//               14.05 / 12.17 / 10.31 ms vs 10.75 ms with the fraction rule alone
+//               (profiles/r4w_shard_threshold.txt)
 // Calibrated at N = 70 only; tests/test_partition.py pins the decisions they produce for the
 // benchmark layouts, so that a recalibration cannot move a layout onto another branch unseen.
 constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kBulkCu = 180e-9, kFwdValu = 370e-9,
-                 kBulkVit = 115e-9, kVitWaveLatV = 700e-9, kMixFwd = 0.92, kMixVit = 0.64;
+                 kBulkVit = 115e-9, kVitWaveLatV = 700e-9, kMixFwd = 0.92, kMixVit = 0.64,
+                 kMixGroupCol = 1.4e-6;
 constexpr int64_t kMixPrio = 512;
 
 // Bins of capacity `cap` (first fit, items longest first): the CUs a set of sequential tasks
@@ -859,16 +865,20 @@ int plan_create_impl(const int64_t* off, int64_t nblocks, double split_frac,
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_URGENT_FRAC")) ufrac = atof(getenv("ITR_URGENT_FRAC"));
 #endif
-  double L = std::max(256.0, ufrac * (double)tmax);
+  // ... and never below what a matrix-core group finishes within the plan's expected makespan
+  // (kMixGroupCol per column of its longest member): a smaller alignment with a short longest
+  // block (a chr100 shard) would otherwise send many blocks to the VALU tasks and reserve CUs
+  // for them that the bulk needs
+  double colns = kMixGroupCol;
 #ifdef ITR_EXPERIMENT
-  // makespan-based threshold: a matrix-core group stepping at ITR_URGENT_COLNS ns per column
-  // must finish its longest member within the plan's expected makespan
-  if (getenv("ITR_URGENT_COLNS")) {
+  if (getenv("ITR_URGENT_COLNS")) colns = atof(getenv("ITR_URGENT_COLNS")) * 1e-9;
+#endif
+  double L = std::max(256.0, ufrac * (double)tmax);
+  if (colns > 0) {
     const int ncu = cus > 0 ? cus : cu_count();
     const double Tm = std::max((double)h_off[nblocks] * kBulkCu / ncu, (double)tmax * kVitLone);
-    L = std::max(256.0, Tm / (atof(getenv("ITR_URGENT_COLNS")) * 1e-9));
+    L = std::max(L, Tm / colns);
   }
-#endif
   std::vector<int32_t> hsplit_blk, utasks, mtasks;
   std::vector<int64_t> ulen;
   struct MT { int32_t id; int64_t steps; bool bwd; };
@@ -1398,9 +1408,10 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     const itr::WaveMfmaGeometry wf = itr::wave_mfma_geometry(m->n);
     // the forward's VALU tasks (halves of the longest blocks) on rf reserved CUs, the long
     // blocks' Viterbi on rv others (plan_partition)
-    const bool split_fwd = fwd_loglik && gf.cfg >= 0 && p->ngroups_ll > 0 && p->nutasks > 0 &&
-                           p->fwd_reserve > 0;
-    bool mixed = split_fwd && wf.mixed && m->EF && p->nmix > 0;
+    const bool hyb_fwd = fwd_loglik && gf.cfg >= 0 && p->ngroups_ll > 0;
+    const bool split_fwd = hyb_fwd && p->nutasks > 0 && p->fwd_reserve > 0;
+    // (the mixed launch also serves a forward without VALU tasks: every half in the groups)
+    bool mixed = hyb_fwd && (split_fwd || p->nutasks == 0) && wf.mixed && m->EF && p->nmix > 0;
 #ifdef ITR_EXPERIMENT
     if (getenv("ITR_NO_MIXED")) mixed = false;
 #endif
@@ -1518,7 +1529,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       HIP_TRY(hipEventRecord(pt->jl2, pt->lng2));
       HIP_TRY(hipStreamWaitEvent(st, pt->jl2, 0));
     }
-    if (split_fwd)  // log P of the split blocks from their two halves
+    if (split_fwd || mixed)  // log P of the split blocks from their two halves
       HIP_TRY(itr::launch_fwd_split_combine(m->n, gf.xr, (int)p->nhsplit, p->d_hsplit_blk,
                                             p->d_svec, p->d_sK, fwd_loglik, st));
   } else if (!few) {
