@@ -73,74 +73,89 @@ def _expo_integral(terms, t):
     return sum(c * _phi(lam, t) for c, lam in terms)
 
 
+def _single_coeffs():
+    """The six coefficient arrays of single_table's integrand (a, b, c, d), without the
+    e^{-mu t} factor of the terms that carry it (flag 1)."""
+    if "single" not in _COEFFS:
+        al = _DELTA[:, None, None, :]   # (a, ., ., d)
+        be = _DELTA.T[None, :, None, :]  # (., b, ., d): delta(d, b)
+        ga = _DELTA.T[None, None, :, :]  # (., ., c, d): delta(d, c)
+        full = lambda x: np.broadcast_to(x, (4, 4, 4, 4)).reshape(-1)  # noqa: E731
+        terms = [(1 / 64, 0, 0), (ga / 16, 1, 1), ((al + be) / 16, 0, -1),
+                 ((al + be) * ga / 4, 1, 0), (al * be / 4, 0, -2), (al * be * ga, 1, -1)]
+        _COEFFS["single"] = (np.stack([full(c) for c, _, _ in terms]),
+                             np.array([f for _, f, _ in terms]),
+                             np.array([m for _, _, m in terms], dtype=np.float64))
+    return _COEFFS["single"]
+
+
+_COEFFS: dict = {}
+
+
 def single_table(t: float, mu: float, k: float) -> np.ndarray:
     """F[a, b, c] = sum_d k/(1-e^{-kt}) int_0^t e^{-ks} P(a,d;s) P(d,b;s) P(d,c;t-s) ds
-    (p_b_c_given_a_JC69_analytical, get_emission_prob_mat.py:73-90)."""
-    al = _DELTA[:, None, None, :]   # (a, ., ., d)
-    be = _DELTA.T[None, :, None, :]  # (., b, ., d): delta(d, b)
-    ga = _DELTA.T[None, None, :, :]  # (., ., c, d): delta(d, c)
+    (p_b_c_given_a_JC69_analytical, get_emission_prob_mat.py:73-90).
+    (1/4 + al x)(1/4 + be x)(1/4 + ga e^{-mu t} / x), x = e^{-mu s}, weight e^{-ks}: six
+    exponential terms whose coefficient arrays are fixed, so one weighted sum of them."""
+    C, flag, mpow = _single_coeffs()
     emt = np.exp(-mu * t)
-    # (1/4 + al x)(1/4 + be x)(1/4 + ga e^{-mu t} / x), x = e^{-mu s}, weight e^{-ks}
-    terms = [
-        (1 / 64, -k),
-        (ga * emt / 16, -k + mu),
-        ((al + be) / 16, -k - mu),
-        ((al + be) * ga * emt / 4, -k),
-        (al * be / 4, -k - 2 * mu),
-        (al * be * ga * emt, -k - mu),
-    ]
-    val = k * _expo_integral(terms, t) / (1 - np.exp(-(k * t)))
-    out = np.zeros((4, 4, 4))
-    for d in range(4):  # sum over d in order, like the reference's cumsum
-        out = out + np.broadcast_to(val, (4, 4, 4, 4))[..., d]
-    return out
+    w = np.where(flag == 1, emt, 1.0) * _phi(-k + mu * mpow, t)
+    val = k * (w @ C) / (1 - np.exp(-(k * t)))
+    return val.reshape(4, 4, 4, 4).sum(axis=3)
+
+
+def _double_coeffs():
+    """The 24 coefficient arrays of double_table's integrand (a, b, c, d, e, f) with their
+    exponents, without the e^{-mu t} factor (flag v = -1)."""
+    if "double" not in _COEFFS:
+        D = _DELTA
+        al = D[:, None, None, None, :, None]          # delta(a, e)
+        be = D.T[None, :, None, None, :, None]        # delta(e, b)
+        ga = D[None, None, None, None, :, :]          # delta(e, f)
+        de = D.T[None, None, :, None, None, :]        # delta(f, c)
+        ep = D.T[None, None, None, :, None, :]        # delta(f, d)
+        A = [(1 / 16, 0), ((al + be) / 4, 1), (al * be, 2)]   # coefficient, power of y1
+        G = [(1 / 4, 0), (ga, 1)]                             # y2^q y1^-q
+        Dl = [(1 / 4, 0), (de, 1)]                            # y2^u
+        Ep = [(1 / 4, 0), (ep, -1)]                           # y2^-v (x e^{-mu t})
+        cs, pq, quv, flag = [], [], [], []
+        for ca, p in A:
+            for cg, q in G:
+                for cd, u in Dl:
+                    for ce, v in Ep:
+                        cs.append(np.broadcast_to(ca * cg * cd * ce, (4,) * 6).reshape(-1))
+                        pq.append(p - q)
+                        quv.append(q + u + v)
+                        flag.append(v == -1)
+        _COEFFS["double"] = (np.stack(cs), np.array(pq, dtype=np.float64),
+                             np.array(quv, dtype=np.float64), np.array(flag))
+    return _COEFFS["double"]
 
 
 def double_table(t: float, mu: float) -> np.ndarray:
     """DD[a, b, c, d] = sum_{e, f} of the two-coalescence integral: (a, b) -> e at s1
     (rate 3), (e, c) -> f at s2 > s1 (rate 1), f -> d over t - s2; normalised by the
     probability that both happen before t (JC69_analytical_integral_double,
-    get_emission_prob_mat.py:93-424, summed as in 427-441)."""
-    # indices (a, b, c, d, e, f)
-    D = _DELTA
-    al = D[:, None, None, None, :, None]          # delta(a, e)
-    be = D.T[None, :, None, None, :, None]        # delta(e, b)
-    ga = D[None, None, None, None, :, :]          # delta(e, f)
-    de = D.T[None, None, :, None, None, :]        # delta(f, c)
-    ep = D.T[None, None, None, :, None, :]        # delta(f, d)
-    # factors in s1, s2:  e^{-2 s1} e^{-s2} (rates 3 then 1: e^{-3 s1} e^{-(s2 - s1)})
-    #   (1/4 + al y1)(1/4 + be y1)          y1 = e^{-mu s1}
-    #   (1/4 + ga y2 / y1)                  y2 = e^{-mu s2}
-    #   (1/4 + de y2)
-    #   (1/4 + ep e^{-mu t} / y2)
+    get_emission_prob_mat.py:93-424, summed as in 427-441).
+    Factors in s1, s2: e^{-2 s1} e^{-s2}, (1/4 + al y1)(1/4 + be y1), (1/4 + ga y2 / y1),
+    (1/4 + de y2), (1/4 + ep e^{-mu t} / y2) with y1 = e^{-mu s1}, y2 = e^{-mu s2}: 24
+    exponential terms with fixed coefficient arrays, one weighted sum of them."""
+    C, pq, quv, flag = _double_coeffs()
     emt = np.exp(-mu * t)
-    A = [(1 / 16, 0), ((al + be) / 4, 1), (al * be, 2)]        # coefficient, power of y1
-    G = [(1 / 4, 0), (ga, 1)]                                  # y2^q y1^-q
-    Dl = [(1 / 4, 0), (de, 1)]                                 # y2^u
-    Ep = [(1 / 4, 0), (ep * emt, -1)]                          # y2^-v
-    total = 0.0
-    for ca, p in A:
-        for cg, q in G:
-            for cd, u in Dl:
-                for ce, v in Ep:
-                    lam1 = -2.0 - mu * (p - q)
-                    lam2 = -1.0 - mu * (q + u + v)
-                    coef = ca * cg * cd * ce
-                    # int_0^t e^{lam2 s2} int_0^{s2} e^{lam1 s1} ds1 ds2
-                    if lam1 != 0.0:
-                        inner = (_phi(lam1 + lam2, t) - _phi(lam2, t)) / lam1
-                    elif lam2 != 0.0:
-                        inner = t * np.exp(lam2 * t) / lam2 - sc.expm1(lam2 * t) / lam2 ** 2
-                    else:
-                        inner = t * t / 2
-                    total = total + coef * inner
+    lam1 = -2.0 - mu * pq
+    lam2 = -1.0 - mu * quv
+    # int_0^t e^{lam2 s2} int_0^{s2} e^{lam1 s1} ds1 ds2 (lam1 = 0 / lam2 = 0: the limits)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        l1 = np.where(lam1 == 0.0, 1.0, lam1)
+        l2 = np.where(lam2 == 0.0, 1.0, lam2)
+        inner = np.where(lam1 != 0.0, (_phi(lam1 + lam2, t) - _phi(lam2, t)) / l1,
+                         np.where(lam2 != 0.0,
+                                  t * np.exp(lam2 * t) / l2 - sc.expm1(lam2 * t) / l2 ** 2,
+                                  t * t / 2))
+    w = np.where(flag, emt, 1.0) * inner
     den = 1 + 0.5 / np.exp(3 * t) - 1.5 / np.exp(t)
-    val = 3 * np.broadcast_to(total, (4, 4, 4, 4, 4, 4)) / den
-    out = np.zeros((4, 4, 4, 4))
-    for e in range(4):
-        for f in range(4):
-            out = out + val[..., e, f]
-    return out
+    val = 3 * (w @ C) / den
+    return val.reshape(4, 4, 4, 4, 16).sum(axis=4)
 
 
 def jc69_rate(mu: float) -> np.ndarray:

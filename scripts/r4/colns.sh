@@ -15,4 +15,12 @@ for C in ${COLNS:-500 800 1100 1400 2000}; do
   ITR_URGENT_COLNS=$C timeout -k 10 300 python bench.py $B > $O/fv_c$C.json 2> $O/fv_c$C.err || { tail $O/fv_c$C.err; exit 1; }
   python scripts/bench_line.py $O/fv_c$C.json "chr10 colns $C"
 done
+
+unset ITR_LIB
+timeout -k 10 300 python -u -m pytest tests/test_gpu_model.py -x -q -m gpu --timeout 200 --timeout-method thread > $O/pytest_model.log 2>&1 || { tail -30 $O/pytest_model.log; exit 1; }
+tail -1 $O/pytest_model.log
+timeout -k 10 300 python bench.py --cpu-1core-cols 0 --host-path 0 --mode optimize > $O/opt.json 2> $O/opt.err || { tail $O/opt.err; exit 1; }
+python scripts/bench_line.py $O/opt.json optimize
+timeout -k 10 200 python3 scripts/prof_build.py 5 8 > $O/prof_build.log 2>&1 || { tail $O/prof_build.log; exit 1; }
+head -3 $O/prof_build.log
 echo done

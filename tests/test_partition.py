@@ -52,10 +52,13 @@ def test_chr10(lib):
 
 
 def test_chr100_single_gpu(lib):
-    """chr100 on one GPU: 50 k blocks, throughput-bound — no long set, per-wave layout."""
+    """chr100 on one GPU: 50 k blocks, throughput-bound — no long set, per-wave layout, and
+    no forward VALU task (every half fits the 70 ms makespan in a matrix-core group: the
+    mixed launch takes the whole forward)."""
     d = info(geometric(100_000_000))
     assert d["wave_ok"] == 1
     assert d["vit_nlong"] == 0 and d["vit_nlong_v"] == 0 and d["vit_reserve"] == 0
+    assert d["fwd_valu_tasks"] == 0 and d["fwd_reserve"] == 0
 
 
 @pytest.mark.parametrize("rank", range(8))
@@ -68,6 +71,8 @@ def test_chr100_world8_shard(lib, rank):
     assert d["wave_ok"] == 1
     assert 20 <= d["vit_nlong"] <= 30
     assert d["vit_reserve"] + d["fwd_reserve"] <= CUS // 2
+    # the makespan floor of the VALU-task threshold (kMixGroupCol): 6-12 forward CUs, not 20-34
+    assert 1 <= d["fwd_reserve"] <= 12
     assert d["vit_nlong_v"] >= d["vit_nlong"]
 
 
