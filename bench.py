@@ -178,7 +178,7 @@ def pmc_traffic(n, mode, tag_hint=""):
             if len(parts) == 2:
                 # the per-wave kernel runs as the bulk launch plus one launch per reserved set
                 # that joins the queue: its per-dispatch average times its launches per call
-                # (the profiled command, scripts/gpu_r3final.sh, makes 3 itr_viterbi calls)
+                # (the profiled command, scripts/r4/final.sh, makes 3 itr_viterbi calls)
                 def per_call(k, v):
                     return v["hbm_bytes_raw"] * (max(1, round(v.get("calls", 3) / 3))
                                                  if "wave_vit_kernel" in k else 1)

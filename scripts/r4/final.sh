@@ -1,9 +1,9 @@
-# Round 3 final tree: every GPU test, smoke, the default bench and configs 3/4/5 + long
+# Round 4 tree: every GPU test, smoke, the default bench and configs 3/4/5 + long
 # blocks, rocprofv3 kernel trace + FETCH/WRITE of the default bench, SQ/MFMA counter passes
 # of the sweep kernels (scripts/prof_sweeps.py); outputs under gpurun_out/$TAG
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-T=${TAG:-r3zf}
+T=${TAG:-r4z}
 O=gpurun_out/$T
 mkdir -p $O/prof
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
@@ -33,4 +33,8 @@ timeout -s KILL 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d $O/sq -o fetch --output-format csv -- $S > $O/sqf.log 2>&1 || { tail $O/sqf.log; exit 1; }
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d $O/sq -o write --output-format csv -- $S > $O/sqw.log 2>&1 || { tail $O/sqw.log; exit 1; }
 python scripts/pmc_summary.py $O/sq $O/pmc.json sweep wave_ hybrid trace combine > $O/pmc_summary.txt 2>&1
+timeout -k 10 300 python bench.py $B --mode vit > $O/vit.json 2> $O/vit.err || { tail $O/vit.err; exit 1; }
+python scripts/bench_line.py $O/vit.json vit
+timeout -k 10 300 python bench.py $B --n-int 7 > $O/fv77.json 2> $O/fv77.err || { tail $O/fv77.err; exit 1; }
+python scripts/bench_line.py $O/fv77.json fv77
 echo done
