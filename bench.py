@@ -196,6 +196,18 @@ def pmc_traffic(n, mode, tag_hint=""):
     return None, "no PMC summary under profiles/ for this kernel"
 
 
+def fv_call_traffic():
+    """HBM bytes per itr_forward_viterbi call (every launch of the call) from the newest
+    committed profiles/r*_fv_call_traffic.json (scripts/fv_traffic.py over the FETCH_SIZE /
+    WRITE_SIZE passes of the default bench command, scripts/r4/final.sh)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fv_call_traffic.json")))
+    if not files:
+        return None, "no per-call PMC traffic under profiles/"
+    d = json.load(open(files[-1]))
+    return d["bytes_per_call"], (f"{os.path.basename(files[-1])}: FETCH_SIZE+WRITE_SIZE of every "
+                                 f"launch of the call ({len(d['per_kernel'])} kernels), raw")
+
+
 def pmc_rates(n):
     """Issue and matrix-core counters of the sweep kernels from the latest committed
     rocprofv3 --pmc summary (scripts/gpu_r3g.sh -> scripts/pmc_summary.py): per kernel the
@@ -631,7 +643,9 @@ def main():
             ideal_ms = pair_ops * cols_local / (fma_peak * 1e12) * 1e3
         dom_ops = (2 if args.mode == "fv" else 1) * pair_ops * cols_local
         achieved = dom_ops / (dom_ms * 1e-3) / 1e12 if dom_ms else 0.0
-        traffic, traffic_note = pmc_traffic(n, dom_mode)
+        default_fv = args.mode == "fv" and n == 70 and not intro and kind == "chr10" and \
+            args.block_len == 0 and args.mbp is None  # (the profiled command's workload)
+        traffic, traffic_note = fv_call_traffic() if default_fv else pmc_traffic(n, dom_mode)
         rates, rates_src = pmc_rates(n)
         cpu = None
         if opt_mode:
