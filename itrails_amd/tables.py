@@ -31,6 +31,22 @@ def _order():
     return [get_idx_state(i) for i in range(NOBS)]
 
 
+_GROUPS = None
+
+
+def _groups():
+    """The 625 symbols grouped by expansion size k (1, 4, 16, 64, 256 N-free columns): per
+    group the symbols and their [S, k] column-index table."""
+    global _GROUPS
+    if _GROUPS is None:
+        by_k = {}
+        for o, idx in enumerate(_order()):
+            by_k.setdefault(len(idx), []).append((o, idx))
+        _GROUPS = [(np.array([o for o, _ in v]), np.stack([idx for _, idx in v]))
+                   for _, v in sorted(by_k.items())]
+    return _GROUPS
+
+
 def build_tables(a, b, pi) -> HmmTables:
     a = np.ascontiguousarray(a, dtype=np.float64)
     b = np.ascontiguousarray(b, dtype=np.float64)
@@ -38,18 +54,15 @@ def build_tables(a, b, pi) -> HmmTables:
     n = a.shape[0]
     if a.shape != (n, n) or b.shape != (n, 256) or pi.shape != (n,):
         raise ValueError(f"bad HMM shapes a{a.shape} b{b.shape} pi{pi.shape}")
-    order = _order()
+    # emit[o] = b[:, order[o]].sum(axis=1) for every symbol, one fancy index + sum per
+    # expansion size: each sum is the same contiguous pairwise reduction over the same k values
+    # as the reference's per-symbol call, so the tables are bit-identical to it
     emit = np.empty((NOBS, n))
-    log_emit = np.empty((NOBS, n))
-    pi_emit = np.empty((NOBS, n))
-    log_pi_emit = np.empty((NOBS, n))
+    for syms, idx in _groups():
+        emit[syms] = b[:, idx].sum(axis=2).T
     with np.errstate(divide="ignore", invalid="ignore"):
-        for o in range(NOBS):
-            e = b[:, order[o]].sum(axis=1)
-            emit[o] = e
-            log_emit[o] = np.log(e)
-            pe = pi * e
-            pi_emit[o] = pe
-            log_pi_emit[o] = np.log(pe)
+        log_emit = np.log(emit)
+        pi_emit = pi * emit
+        log_pi_emit = np.log(pi_emit)
         log_a = np.log(a)
     return HmmTables(n, a, np.ascontiguousarray(log_a), emit, log_emit, pi_emit, log_pi_emit)
