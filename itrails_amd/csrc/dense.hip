@@ -407,6 +407,74 @@ __global__ void __launch_bounds__(256) panel_kernel(int n, double* Mb, int* pivb
   }
 }
 
+// panel_kernel with the panel (rows [k0, n) x kb columns) held in LDS for the whole
+// factorisation: one global read and one write of the panel instead of a global round trip
+// per column step (the (5,5) build's single LU of Q, n = 201: the column steps are latency-
+// bound).  Same operations in the same order as panel_kernel: bit-identical factors.
+constexpr int kPanelLdsBytes = 60 * 1024;
+__global__ void __launch_bounds__(256) panel_lds_kernel(int n, double* Mb, int* pivb, int k0,
+                                                        int kb) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
+  __shared__ double rv[256];
+  __shared__ int ri[256];
+  double* P = reinterpret_cast<double*>(psm);  // [n - k0][kb]
+  double* M = Mb + (int64_t)blockIdx.x * n * n;
+  int* piv = pivb + (int64_t)blockIdx.x * n;
+  const int tid = threadIdx.x;
+  const int rows = n - k0;
+  for (int e = tid; e < rows * kb; e += 256) {
+    const int r = e / kb, c = e % kb;
+    P[e] = M[(int64_t)(k0 + r) * n + k0 + c];
+  }
+  __syncthreads();
+  for (int jj = 0; jj < kb; ++jj) {
+    const int j = k0 + jj;
+    double bv = -1.0;
+    int bi = j;
+    for (int i = j + tid; i < n; i += 256) {
+      const double v = fabs(P[(i - k0) * kb + jj]);
+      if (v > bv) {
+        bv = v;
+        bi = i;
+      }
+    }
+    rv[tid] = bv;
+    ri[tid] = bi;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+      if (tid < h) {
+        const double o = rv[tid + h];
+        const int oi = ri[tid + h];
+        if (o > rv[tid] || (o == rv[tid] && oi < ri[tid])) {
+          rv[tid] = o;
+          ri[tid] = oi;
+        }
+      }
+      __syncthreads();
+    }
+    const int p = ri[0];
+    if (tid == 0) piv[j] = p;
+    if (p != j && tid < kb) {
+      const double t = P[jj * kb + tid];
+      P[jj * kb + tid] = P[(p - k0) * kb + tid];
+      P[(p - k0) * kb + tid] = t;
+    }
+    __syncthreads();
+    const double rd = 1.0 / P[jj * kb + jj];
+    for (int i = j + 1 + tid; i < n; i += 256) {
+      double* row = P + (i - k0) * kb;
+      const double lij = row[jj] * rd;
+      row[jj] = lij;
+      for (int c = jj + 1; c < kb; ++c) row[c] -= lij * P[jj * kb + c];
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < rows * kb; e += 256) {
+    const int r = e / kb, c = e % kb;
+    M[(int64_t)(k0 + r) * n + k0 + c] = P[e];
+  }
+}
+
 // Apply the panel's row interchanges to every column outside the panel (and to R).
 __global__ void __launch_bounds__(256) swap_kernel(int n, int nrhs, double* Mb, double* Rb,
                                                    const int* pivb, int k0, int kb) {
@@ -514,7 +582,11 @@ hipError_t solve_batched(int n, int nrhs, int64_t batch, double* M, double* R, i
     int* pc = piv + b0 * n;
     for (int k0 = 0; k0 < n; k0 += NB) {
       const int kb = std::min(NB, n - k0), k1 = k0 + kb;
-      hipLaunchKernelGGL(panel_kernel, dim3(nb), dim3(256), 0, st, n, Mc, pc, k0, kb);
+      const size_t pbytes = (size_t)(n - k0) * kb * sizeof(double);
+      if (pbytes <= (size_t)kPanelLdsBytes)
+        hipLaunchKernelGGL(panel_lds_kernel, dim3(nb), dim3(256), pbytes, st, n, Mc, pc, k0, kb);
+      else
+        hipLaunchKernelGGL(panel_kernel, dim3(nb), dim3(256), 0, st, n, Mc, pc, k0, kb);
       hipLaunchKernelGGL(swap_kernel, dim3((n + nrhs + 255) / 256, nb), dim3(256), 0, st, n,
                          nrhs, Mc, Rc, pc, k0, kb);
       const int right = n - k1;
