@@ -394,18 +394,20 @@ __global__ void __launch_bounds__(256) post_combine_kernel(int n, int xr, const 
   const double* b = beta + (beta_off[blk] + t) * xr;
   const double q0 = l < n ? a[l] * b[l] : 0.0;
   const double q1 = l + 64 < n ? a[l + 64] * b[l + 64] : 0.0;
-  const double S = wave_sum(q0 + q1);
+  const double q2 = l + 128 < n ? a[l + 128] * b[l + 128] : 0.0;  // (n <= 192)
+  const double S = wave_sum((q0 + q1) + q2);
   const double rS = 1.0 / S;
   double* dst = post + (c0 + t) * n;
   if (l < n) dst[l] = q0 * rS;
   if (l + 64 < n) dst[l + 64] = q1 * rS;
+  if (l + 128 < n) dst[l + 128] = q2 * rS;
 }
 
 hipError_t launch_post_combine(int n, int xr, int nlong, int64_t tmax, const int32_t* order,
                                const int64_t* off, const double* alpha, const double* beta,
                                const int64_t* beta_off, double* post, hipStream_t st) {
   if (nlong <= 0 || tmax <= 0) return hipSuccess;
-  if (n > 128) return hipErrorInvalidValue;
+  if (n > 192) return hipErrorInvalidValue;
   hipLaunchKernelGGL(post_combine_kernel, dim3((unsigned)((tmax + 3) / 4), (unsigned)nlong),
                      dim3(256), 0, st, n, xr, order, off, alpha, beta, beta_off, post);
   return hipGetLastError();
