@@ -1330,6 +1330,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     return ta;
   };
   int64_t traced = 0;
+  int64_t trace_end = p->nblocks;  // the final traceback walks order[traced, trace_end)
   const itr::WaveVitGeometry wv = itr::wave_vit_geometry(m->n);
   bool wave = wv.iq > 0 && m->xrw == wv.xr;
   const int cus = cu_count();
@@ -1395,6 +1396,9 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     w.lpie = m->LPIE;
     w.slot_state = m->VSLOT;
     w.slot_m = m->VMB;
+    w.log_e = m->LE;  // each bulk block traced by its wave right after its sweep
+    w.path = path;
+    trace_end = nlong;
     w.ckpt = p->d_alpha;
     w.stay = p->d_stay;
     w.last_state = p->d_last;
@@ -1537,7 +1541,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   }
   both.reset();
   itr::TraceArgs ta = trace_args();
-  ta.nblocks = p->nblocks - traced;
+  ta.nblocks = std::max<int64_t>(0, trace_end - traced);
   ta.order = p->d_order + traced;
   // one wave per block, 4 waves per workgroup (LDS: 4 x 16 recomputed rows)
   const int64_t grid = std::min<int64_t>((ta.nblocks + 3) / 4, (int64_t)cu_count() * 4);

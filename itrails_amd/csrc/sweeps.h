@@ -129,6 +129,9 @@ struct VitArgs {
   const double* lpie;           // log(pi E), 625 x n
   const int32_t* slot_state;    // [xr] state of each slot (-1: padding), wave_tasks.h
   const double* slot_m;         // [xr] max_{i != j} log a_ij of the slot's state j
+  // non-null: the wave traces each block right after its sweep (trace.h) into `path`
+  const double* log_e;          // 625 x n (state order)
+  uint8_t* path;                // [total]
   double* ckpt;                 // [tiles x xr]
   uint16_t* stay;               // [tiles x xr]
   uint8_t* last_state;          // [plan blocks]

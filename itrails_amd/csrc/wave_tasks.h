@@ -67,6 +67,7 @@
 #include <stdint.h>
 
 #include "sweeps.h"
+#include "trace.h"
 #include "valu_sweep.h"
 
 namespace itr {
@@ -153,6 +154,31 @@ __device__ __forceinline__ double row16_sum_w(double v) {
   v += dpp_f64<0x4E>(v);
   v += dpp_f64<0x141>(v);
   return v + dpp_f64<0x128>(v);
+}
+
+// The block's traceback by the wave that swept it (VitArgs.path non-null): its checkpoint
+// rows and flag words were stored by this wave's buffer stores, so they are made visible to
+// its own loads first (release: wait for the stores; acquire: drop the vector L1's lines),
+// and the wave's LDS region is free for the traceback's tile rows once the last staging DMA
+// has landed (the release waits for it too).
+template <int XRW>
+__device__ __forceinline__ void vit_wave_trace(const VitArgs& p, double* wl, int blk, int s) {
+  static_assert(VIT_TILE * XRW <= 144 + 2 * 640, "the tile rows fit the wave's LDS region");
+  if (p.path == nullptr) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  TraceArgs ta{};
+  ta.n = p.n;
+  ta.xr = p.xr;
+  ta.off = p.off;
+  ta.tile_off = p.tile_off;
+  ta.obs = p.obs;
+  ta.log_a = p.la;
+  ta.log_e = p.log_e;
+  ta.ckpt = p.ckpt;
+  ta.stay = p.stay;
+  ta.path = p.path;
+  trace_block<(XRW + 63) / 64>(ta, wl, blk, s);
 }
 
 // maximum over the wave, uniform (every lane's value counts)
@@ -380,6 +406,7 @@ __device__ __forceinline__ void vit_wave_task(const VitArgs& p, double* wl, int 
     }
     wave_first_max(bv, bj);
     if (l == 0) p.last_state[blk] = (uint8_t)bj;
+    vit_wave_trace<XRW>(p, wl, blk, uni(bj));
     if (urgent) __builtin_amdgcn_s_setprio(0);
   }
 }
@@ -589,6 +616,7 @@ __device__ __forceinline__ void vit_wave_task_full(const VitArgs& p, double* wl,
     }
     wave_first_max(bv, bj);
     if (l == 0) p.last_state[blk] = (uint8_t)bj;
+    vit_wave_trace<XRW>(p, wl, blk, uni(bj));
     if (urgent) __builtin_amdgcn_s_setprio(0);
   }
 }
