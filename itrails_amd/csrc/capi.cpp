@@ -1545,7 +1545,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   ta.order = p->d_order + traced;
   // one wave per block, 4 waves per workgroup (LDS: 4 x 16 recomputed rows)
   const int64_t grid = std::min<int64_t>((ta.nblocks + 3) / 4, (int64_t)cu_count() * 4);
-  HIP_TRY(hipMemsetAsync(ta.queue, 0, sizeof(int), st));
+  if (ta.nblocks > 0) HIP_TRY(hipMemsetAsync(ta.queue, 0, sizeof(int), st));
   Scope sc("traceback", st);
   if (ta.nblocks > 0) HIP_TRY(itr::launch_vit_traceback(ta, (int)grid, st));
   return 0;

@@ -33,6 +33,7 @@ timeout -s KILL 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d $O/sq -o fetch --output-format csv -- $S > $O/sqf.log 2>&1 || { tail $O/sqf.log; exit 1; }
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d $O/sq -o write --output-format csv -- $S > $O/sqw.log 2>&1 || { tail $O/sqw.log; exit 1; }
 python scripts/pmc_summary.py $O/sq $O/pmc.json sweep wave_ hybrid trace combine > $O/pmc_summary.txt 2>&1
+python scripts/fv_traffic.py $O/prof $O/fv_call_traffic.json > /dev/null
 timeout -k 10 300 python bench.py $B --mode vit > $O/vit.json 2> $O/vit.err || { tail $O/vit.err; exit 1; }
 python scripts/bench_line.py $O/vit.json vit
 timeout -k 10 300 python bench.py $B --n-int 7 > $O/fv77.json 2> $O/fv77.err || { tail $O/fv77.err; exit 1; }
