@@ -93,10 +93,18 @@ ITR_API int itr_plan_create(const int64_t* h_block_off, int64_t n_blocks, itr_pl
 ITR_API int itr_plan_create_ex(const int64_t* h_block_off, int64_t n_blocks, double split_frac,
                                double post_split_frac, itr_plan_t* out);
 ITR_API int itr_plan_destroy(itr_plan_t plan);
+/* The per-wave Viterbi (N = 65..72) decodes a block with one of two steps that give the same
+ * bits: a bound-pruned step (fewer instructions per column) for blocks shorter than a planned
+ * length, a full scan (shorter dependent chain) for the others.  Blocks shorter than `len`
+ * take the pruned step in every later call on this plan (0: never, INT64_MAX: always;
+ * negative: back to the planned lengths, see itr_plan_partition_info). */
+ITR_API int itr_plan_set_prune_len(itr_plan_t plan, int64_t len);
 /* The plan's work placement on a device with `cus` compute units, host-side only (no device
- * needed): out[0..7] = forward+Viterbi long set (blocks, columns), its reserved CUs, the
+ * needed): out[0..9] = forward+Viterbi long set (blocks, columns), its reserved CUs, the
  * forward's reserved CUs, per-wave layout on (1/0), the Viterbi-only call's long set, the
- * forward's VALU tasks, the mixed queue's entries.  For tests and diagnostics. */
+ * forward's VALU tasks, the mixed queue's entries, the block length below which the per-wave
+ * Viterbi takes the bound-pruned step (forward+Viterbi call, Viterbi-only call).  For tests
+ * and diagnostics. */
 ITR_API int itr_plan_partition_info(const int64_t* h_block_off, int64_t n_blocks, int cus,
                                     int64_t* out);
 ITR_API int itr_plan_total_columns(itr_plan_t plan, int64_t* total);

@@ -37,6 +37,7 @@ _SIGNATURES = {
     "itr_plan_create_ex": ([_P, _I64, _D, _D, ctypes.POINTER(_P)], _I),
     "itr_plan_destroy": ([_P], _I),
     "itr_plan_partition_info": ([_P, _I64, _I, _P], _I),
+    "itr_plan_set_prune_len": ([_P, _I64], _I),
     "itr_plan_total_columns": ([_P, ctypes.POINTER(_I64)], _I),
     "itr_plan_reserve": ([_P, _I, _I], _I),
     "itr_forward_loglik": ([_P, _P, _P, _P, _P], _I),

@@ -249,10 +249,12 @@ struct itr_model {
   double *a = nullptr, *la = nullptr, *E = nullptr, *LE = nullptr, *PIE = nullptr,
          *LPIE = nullptr, *aT = nullptr;
   // the one-block-per-wave Viterbi (wave_tasks.h), when that layout serves this state count
-  // (xrw = its slot count): log E in slot order padded to xrw columns (-inf), the state of
-  // every slot, max_{i != j} log a_ij per slot; built on the model's first Viterbi call
-  // (vit_slot_tables) from host copies of the tables kept until then
+  // (xrw = its slot count): log E padded to xrw columns (-inf) by state (the full-scan step)
+  // and in the bound-pruned step's slot order, the state of every slot, max_{i != j} log a_ij
+  // per slot; built on the model's first Viterbi call (vit_slot_tables) from host copies of
+  // the tables kept until then
   double* LEW = nullptr;
+  double* LEWP = nullptr;
   int32_t* VSLOT = nullptr;
   double* VMB = nullptr;
   int xrw = 0;
@@ -307,6 +309,10 @@ struct itr_plan {
   bool wave_ok = true;
   int32_t* d_mix = nullptr;
   int mix_prio_fwd = INT32_MAX, mix_prio_vit = INT32_MAX;
+  // per-wave Viterbi: blocks shorter than this take the bound-pruned step (wave_tasks.h), in
+  // the forward+Viterbi and the Viterbi-only call
+  int vit_prune_len = 0, vit_prune_len_v = 0;
+  int64_t prune_override = -1;  // itr_plan_set_prune_len (negative: the planned lengths)
   int64_t nutasks = 0, ngroups_ll = 0, nhsplit = 0;
   int32_t *d_utasks = nullptr, *d_mtasks = nullptr, *d_groups_ll = nullptr,
           *d_hsplit_blk = nullptr;
@@ -365,6 +371,14 @@ int vit_stride(int n) {
 //               load at N = 70 of a matrix-core forward group (~0.92 us) and a per-wave Viterbi
 //               block (~0.64 us), measured on chr10 (profiles/r3l_*)
 //   kMixPrio    mixed-queue entries that run at raised wave priority: about one per SIMD pair
+//   kPruneCol   a per-wave Viterbi block takes the bound-pruned step (fewer instructions per
+//               column, a longer dependent chain: wave_tasks.h) when its length x kPruneCol
+//               fits within the expected makespan, the full scan otherwise; chr10
+//               forward+Viterbi with 1.0 / 1.4 / 2.0 / 2.9 / 4.0 / 6.0 us and all blocks on the
+//               full scan: 7.95-7.99 / 7.64-7.65 / 7.67-7.73 / 7.82 / 7.85 / 7.94 / 8.12 ms per
+//               step; chr100 (every block pruned) 59.4 -> 51.6 ms, its world-8 shards 8.96 ->
+//               8.61 ms; the Viterbi-only call stays at its long set's floor (6.1 ms)
+//               (profiles/r4pc_prune_col.txt)
 //   kMixGroupCol  the per-column step a forward half may take in a matrix-core group and
 //               still finish within the expected makespan (sets the floor of the VALU-task
 //               threshold): chr100 world-8 shards with 0.7 / 1.0 / 1.4 us -> slowest shard
@@ -374,7 +388,7 @@ int vit_stride(int n) {
 // benchmark layouts, so that a recalibration cannot move a layout onto another branch unseen.
 constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kBulkCu = 180e-9, kFwdValu = 370e-9,
                  kBulkVit = 115e-9, kVitWaveLatV = 700e-9, kMixFwd = 0.92, kMixVit = 0.64,
-                 kMixGroupCol = 1.4e-6;
+                 kMixGroupCol = 1.4e-6, kPruneCol = 1.4e-6;
 constexpr int64_t kMixPrio = 512;
 
 // Bins of capacity `cap` (first fit, items longest first): the CUs a set of sequential tasks
@@ -433,13 +447,19 @@ void plan_partition(itr_plan_t p, const std::vector<int64_t>& ulen, int cus) {
   while (kv < nblocks && p->sorted_len[kv] >= 2048 && (double)p->sorted_len[kv] * kVitWaveLatV > Tv)
     ++kv;
   p->vit_nlong_v = kv;
+  // the per-wave Viterbi's step per block: bound-pruned below these lengths (kPruneCol)
+  double pcol = kPruneCol;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_VIT_NLONG_V")) p->vit_nlong_v = atoi(getenv("ITR_VIT_NLONG_V"));
+  if (getenv("ITR_PRUNE_COL")) pcol = atof(getenv("ITR_PRUNE_COL"));
 #endif
+  p->vit_prune_len = (int)std::min(T / pcol, (double)INT32_MAX);
+  p->vit_prune_len_v = (int)std::min(Tv / pcol, (double)INT32_MAX);
   if (getenv("ITR_VERBOSE"))
-    fprintf(stderr, "[itr] partition: T %.3f ms, long %lld blocks (%lld cols), rv %d rf %d (%zu halves)%s\n",
+    fprintf(stderr, "[itr] partition: T %.3f ms, long %lld blocks (%lld cols), rv %d rf %d (%zu halves)%s, "
+            "pruned below %d / %d columns\n",
             T * 1e3, (long long)k, (long long)cols, p->vit_reserve, rf, halves.size(),
-            p->wave_ok ? "" : ", no wave layout");
+            p->wave_ok ? "" : ", no wave layout", p->vit_prune_len, p->vit_prune_len_v);
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_VIT_RESERVE")) p->vit_reserve = atoi(getenv("ITR_VIT_RESERVE"));
   if (getenv("ITR_FWD_RESERVE")) p->fwd_reserve = atoi(getenv("ITR_FWD_RESERVE"));
@@ -711,6 +731,7 @@ int itr_model_destroy(itr_model_t m) {
   dev_free(m->LPIE);
   dev_free(m->aT);
   dev_free(m->LEW);
+  dev_free(m->LEWP);
   dev_free(m->VSLOT);
   dev_free(m->VMB);
   dev_free(m->EF);
@@ -1047,7 +1068,15 @@ int itr_plan_partition_info(const int64_t* off, int64_t nblocks, int cus, int64_
   out[5] = p->vit_nlong_v;
   out[6] = p->nutasks;
   out[7] = p->nmix;
+  out[8] = p->vit_prune_len;
+  out[9] = p->vit_prune_len_v;
   delete p;  // (host-only: nothing on the device)
+  return 0;
+}
+
+int itr_plan_set_prune_len(itr_plan_t p, int64_t len) {
+  if (int e = check_plan(p)) return e;
+  p->prune_override = len < 0 ? -1 : len;
   return 0;
 }
 
@@ -1184,7 +1213,6 @@ int vit_slot_tables(itr_model_t m) {
       if (i != j) mj[j] = std::max(mj[j], la[(size_t)i * n + j]);
   std::vector<int> rank(n);
   std::iota(rank.begin(), rank.end(), 0);
-#ifdef ITR_VIT_PRUNED
   std::vector<int64_t> fails(n, 0);
   uint64_t rs = 0x2545F4914F6CDD1Dull;
   auto rnd = [&]() {  // splitmix64 -> [0, 1)
@@ -1233,51 +1261,34 @@ int vit_slot_tables(itr_model_t m) {
   std::vector<int32_t> slot(w, -1);
   for (int k = 0; k < n; ++k)
     slot[k < 8 * (iq - 1) ? iq * (k % 8) + k / 8 : iq * (k - 8 * (iq - 1)) + iq - 1] = rank[k];
-#else
-  std::vector<int32_t> slot(w, -1);  // the full-scan step: slot = state
-  for (int sl = 0; sl < n; ++sl) slot[sl] = rank[sl];
-#endif
-  std::vector<double> lew((size_t)ITR_NOBS * w, -INFINITY), vmb(w, -INFINITY);
+  // log E padded to w columns: by state (full scan) and by slot (pruned step)
+  std::vector<double> lew((size_t)ITR_NOBS * w, -INFINITY), lewp(lew.size(), -INFINITY),
+      vmb(w, -INFINITY);
+  for (int o = 0; o < ITR_NOBS; ++o)
+    for (int j = 0; j < n; ++j) lew[(size_t)o * w + j] = m->h_LE[(size_t)o * n + j];
   for (int sl = 0; sl < w; ++sl) {
     if (slot[sl] < 0) continue;
     vmb[sl] = mj[slot[sl]];
-    for (int o = 0; o < ITR_NOBS; ++o) lew[(size_t)o * w + sl] = m->h_LE[(size_t)o * n + slot[sl]];
+    for (int o = 0; o < ITR_NOBS; ++o) lewp[(size_t)o * w + sl] = m->h_LE[(size_t)o * n + slot[sl]];
   }
   int e = dev_alloc(&m->VSLOT, (size_t)w);
   if (!e) e = dev_alloc(&m->VMB, (size_t)w);
   if (!e) e = dev_alloc(&m->LEW, lew.size());
+  if (!e) e = dev_alloc(&m->LEWP, lewp.size());
   if (!e && (hipMemcpy(m->VSLOT, slot.data(), w * sizeof(int32_t), hipMemcpyHostToDevice) != hipSuccess ||
              hipMemcpy(m->VMB, vmb.data(), w * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
-             hipMemcpy(m->LEW, lew.data(), lew.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess))
+             hipMemcpy(m->LEW, lew.data(), lew.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+             hipMemcpy(m->LEWP, lewp.data(), lewp.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess))
     e = fail(ITR_EHIP, "table upload failed");
   if (e) {
     dev_free(m->VSLOT);
     dev_free(m->VMB);
     dev_free(m->LEW);
-    m->VSLOT = nullptr;
-    m->VMB = nullptr;
-    m->LEW = nullptr;
+    dev_free(m->LEWP);
     return e;
   }
   for (auto* v : {&m->h_a, &m->h_la, &m->h_LE, &m->h_E, &m->h_PIE}) std::vector<double>().swap(*v);
   return 0;
-}
-
-itr::TraceArgs trace_args(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path) {
-  itr::TraceArgs ta{};
-  ta.n = m->n;
-  ta.xr = vit_stride(m->n);
-  ta.off = p->d_off;
-  ta.tile_off = p->d_tile_off;
-  ta.queue = p->d_queue + 1;
-  ta.obs = obs;
-  ta.log_a = m->la;
-  ta.log_e = m->LE;
-  ta.ckpt = p->d_alpha;
-  ta.stay = p->d_stay;
-  ta.last_state = p->d_last;
-  ta.path = path;
-  return ta;
 }
 
 // The Viterbi sweep and traceback of every block into `path`; with fwd_loglik, the forward
@@ -1396,6 +1407,13 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     w.lpie = m->LPIE;
     w.slot_state = m->VSLOT;
     w.slot_m = m->VMB;
+    w.lew_p = m->LEWP;
+    w.prune_len = p->prune_override >= 0
+                      ? (int)std::min<int64_t>(p->prune_override, INT32_MAX)
+                      : (vonly ? p->vit_prune_len_v : p->vit_prune_len);
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_PRUNE_LEN")) w.prune_len = atoi(getenv("ITR_PRUNE_LEN"));
+#endif
     w.log_e = m->LE;  // each bulk block traced by its wave right after its sweep
     w.path = path;
     trace_end = nlong;

@@ -125,10 +125,13 @@ struct VitArgs {
   const int64_t* tile_off;      // [plan blocks + 1]
   const uint16_t* obs;          // [total]
   const double* la;             // log a, n x n
-  const double* lew;            // log E, 625 x xr, columns in slot order (padding: -inf)
+  const double* lew;            // log E, 625 x xr, by state (padding: -inf): full-scan step
   const double* lpie;           // log(pi E), 625 x n
-  const int32_t* slot_state;    // [xr] state of each slot (-1: padding), wave_tasks.h
+  // the bound-pruned step (wave_tasks.h): its slot order and log E in that order
+  const int32_t* slot_state;    // [xr] state of each slot (-1: padding)
   const double* slot_m;         // [xr] max_{i != j} log a_ij of the slot's state j
+  const double* lew_p;          // log E, 625 x xr, columns in slot order (padding: -inf)
+  int prune_len;                // blocks shorter than this take the bound-pruned step
   // non-null: the wave traces each block right after its sweep (trace.h) into `path`
   const double* log_e;          // 625 x n (state order)
   uint8_t* path;                // [total]

@@ -13,15 +13,8 @@
 namespace itr {
 namespace {
 
-#ifdef ITR_VIT_PRUNED
 template <int IQ>
-using VitLayout = WaveVit<IQ>;
-#define ITR_VIT_TASK vit_wave_task
-#else
-template <int IQ>
-using VitLayout = WaveVitFull<IQ>;
-#define ITR_VIT_TASK vit_wave_task_full
-#endif
+using VitLayout = WaveVitAny<IQ>;
 
 constexpr int kWaves = 4;  // independent wavefronts per workgroup
 
@@ -41,7 +34,7 @@ __global__ void __launch_bounds__(64 * kWaves, 2) wave_vit_kernel(VitArgs p) {
   for (;;) {
     const int bi = next_task(p.queue);
     if (bi >= p.nblocks) break;
-    ITR_VIT_TASK<IQ>(p, wl, uni(p.order[bi]));
+    vit_wave_block<IQ>(p, wl, uni(p.order[bi]));
   }
 }
 
@@ -76,7 +69,7 @@ __global__ void __launch_bounds__(64 * kWaves, 2)
     if (e < 0) {
       fwd_wave_task<NT, NK>(f, wl, -e - 1);
     } else {
-      ITR_VIT_TASK<IQ>(v, wl, e);
+      vit_wave_block<IQ>(v, wl, e);
     }
   }
 }

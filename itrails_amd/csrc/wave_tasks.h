@@ -7,13 +7,21 @@
 // ---- Viterbi, one block per wavefront ----------------------------------------------------
 //
 // One wavefront decodes a whole block on its own (no workgroup barrier; a wave's LDS
-// instructions execute in order).  The states are laid out in 8 IQ slots (IQ = 9: 72 slots
-// for N = 65..72), slot s = IQ g + r holding the state VSLOT[s] (the model's slot order,
-// capi.cpp vit_slot_tables).  Lane l = 8 g + q holds, in VGPRs, log a between the source
-// slots of chunk q (IQ q .. IQ q + IQ - 1) and the target slots of group g, and owns target
-// slot IQ g + q (A) and, for q = 0, target slot IQ g + IQ - 1 (B).
+// instructions execute in order), by one of two steps chosen per block (vit_wave_block):
 //
-// Bound-pruned step (exact).  With Omega = max_i omega_i (a wave-wide maximum) and
+// Full scan (vit_wave_task_full, blocks at least p.prune_len long): lane l = 8 q + g holds,
+// in VGPRs, log a between sources IQ q .. IQ q + IQ - 1 and targets IQ g .. IQ g + IQ - 1,
+// forms 9 partial maxima, writes them to the wave's partial table in LDS and finalises
+// target l (and, lanes 0-7, 64 + l) from its 8 partials: ~181 VALU instructions per column,
+// the shortest dependent chain — the step for the blocks whose latency sets the makespan.
+//
+// Bound-pruned step (vit_wave_task, the shorter blocks: fewer instructions per column, a
+// longer chain).  The states are laid out in 8 IQ slots (IQ = 9: 72 slots for N = 65..72),
+// slot s = IQ g + r holding the state VSLOT[s] (the model's slot order, capi.cpp
+// vit_slot_tables).  Lane l = 8 g + q holds, in VGPRs, log a between the source slots of
+// chunk q (IQ q .. IQ q + IQ - 1) and the target slots of group g, and owns target slot
+// IQ g + q (A) and, for q = 0, target slot IQ g + IQ - 1 (B).
+// With Omega = max_i omega_i (a wave-wide maximum) and
 // M_j = max_{i != j} log a_ij (per model), rounding is monotone, so for every i != j
 //   fl(fl(omega_i + log a_ij) + log e_j) <= fl(fl(Omega + M_j) + log e_j) =: B_j.
 // A target whose stay score yd = fl(fl(omega_j + log a_jj) + log e_j) exceeds B_j has
@@ -29,11 +37,12 @@
 //
 // Outputs are those of the VALU sweep — the omega row of every 16-column tile's first column,
 // 16-bit stay-flag words, the last column's first argmax (by state index) — so the
-// traceback (hmm_sweeps.hip) is shared and paths are bit-identical.  The emission rows
-// (slot order, padded to 8 IQ) are staged 8 columns at a time into the wave's LDS ring by
-// direct-to-LDS loads.  Two waves share a SIMD; itr_viterbi gives the longest blocks to the
-// 9-wave VALU layout on a reserved set of CUs and this kernel the rest (capi.cpp, DESIGN.md
-// §3.4); blocks at least p.prio_len long run at raised wave priority.
+// traceback (trace.h) is shared and paths are bit-identical whichever step ran.  The
+// emission rows (padded to 8 IQ; slot order for the pruned step) are staged 8 columns at a
+// time into the wave's LDS ring by direct-to-LDS loads.  Two waves share a SIMD; itr_viterbi
+// gives the longest blocks to the 9-wave VALU layout on a reserved set of CUs and this
+// kernel the rest (capi.cpp); blocks at least p.prio_len long run at raised
+// wave priority.
 //
 // ---- forward log-likelihood, four tasks per wavefront on the matrix cores ----------------
 //
@@ -255,7 +264,7 @@ __device__ __forceinline__ void vit_wave_task(const VitArgs& p, double* wl, int 
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
         const int e = 128 * i + 2 * l;
-        const double* src = p.lew;
+        const double* src = p.lew_p;
         if (e < HT * XRW) src += (int64_t)sym(h * HT + e / XRW) * XRW + e % XRW;
         __builtin_amdgcn_global_load_lds(
             src, (__attribute__((address_space(3))) void*)(d + 128 * i), 16, 0, 0);
@@ -411,10 +420,8 @@ __device__ __forceinline__ void vit_wave_task(const VitArgs& p, double* wl, int 
   }
 }
 
-#ifndef ITR_VIT_PRUNED
-// The full-scan per-wave step (the product step until the bound-pruned one above, built with
-// -DITR_VIT_PRUNED, is faster): lane l = 8 q + g, partial table in LDS, slots = states
-// (capi.cpp builds the identity slot order for it).
+// The full-scan per-wave step: lane l = 8 q + g, partial table in LDS, states in their own
+// order (p.lew by state).
 template <int IQ>
 struct WaveVitFull {
   static constexpr int XRW = 8 * IQ;                  // targets = sources of the layout
@@ -621,7 +628,23 @@ __device__ __forceinline__ void vit_wave_task_full(const VitArgs& p, double* wl,
   }
 }
 
-#endif
+// One Viterbi block on this wave: the bound-pruned step for blocks shorter than p.prune_len,
+// the full scan for the others.  The two layouts carve the wave's LDS region differently, so
+// a staging DMA still in flight from the wave's previous task (any kind) lands first.
+template <int IQ>
+struct WaveVitAny {
+  static constexpr int WL =
+      WaveVit<IQ>::WL > WaveVitFull<IQ>::WL ? WaveVit<IQ>::WL : WaveVitFull<IQ>::WL;
+};
+template <int IQ>
+__device__ __forceinline__ void vit_wave_block(const VitArgs& p, double* wl, int blk) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int T = uni((int)(p.off[blk + 1] - p.off[blk]));
+  if (T < p.prune_len)
+    vit_wave_task<IQ>(p, wl, blk);
+  else
+    vit_wave_task_full<IQ>(p, wl, blk);
+}
 
 template <int NT, int NK>
 __device__ __forceinline__ void fwd_wave_task(const WaveMfmaArgs& p, double* wl, int gi) {

@@ -117,6 +117,11 @@ class Plan:
     def reserve(self, n: int, posterior: bool = False):
         check(lib().itr_plan_reserve(self.handle, n, int(posterior)))
 
+    def set_prune_len(self, length=None):
+        """Per-wave Viterbi step choice (itr_plan_set_prune_len): blocks shorter than `length`
+        take the bound-pruned step; None = the planned lengths."""
+        check(lib().itr_plan_set_prune_len(self.handle, -1 if length is None else int(length)))
+
     def close(self):
         if getattr(self, "handle", None):
             lib().itr_plan_destroy(self.handle)

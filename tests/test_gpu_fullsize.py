@@ -101,6 +101,19 @@ def test_full_size_forward_viterbi_every_block(full):
     _check_all_blocks(full["t"], full["obs"], full["off"], ll, path)
 
 
+@pytest.mark.parametrize("prune", [0, 1 << 62])
+def test_full_size_viterbi_either_step(full, prune):
+    """The per-wave Viterbi with every bulk block on the full scan, and on the bound-pruned
+    step (itr_plan_set_prune_len): the same 10 M-column path, bit for bit, as the planned mix
+    (checked against the CPU restatement on every block above)."""
+    plan = hmm.Plan(full["off"])
+    plan.set_prune_len(prune)
+    _, path = hmm.forward_viterbi_device(full["model"], plan, full["d_obs"])
+    assert np.array_equal(path.cpu().numpy(), full["path"])
+    path = hmm.viterbi_device(full["model"], plan, full["d_obs"])
+    assert np.array_equal(path.cpu().numpy(), full["path"])
+
+
 @pytest.mark.parametrize("rank", range(8))
 def test_chr100_shard_forward_viterbi(gpu, rank):
     """BASELINE config 4's per-rank work at world size 8: every shard of the fixed 100 Mbp

@@ -84,13 +84,19 @@ def test_ties_first_maximum(gpu):
     np.testing.assert_array_equal(hmm._paths(model, plan, obs), O.viterbi(t, obs, off))
 
 
+# per-wave Viterbi step choice (itr_plan_set_prune_len): planned lengths, every block on the
+# full scan, every block on the bound-pruned step
+PRUNE = [None, 0, 1 << 62]
+
+
+@pytest.mark.parametrize("prune", PRUNE)
 @pytest.mark.parametrize("combined", [False, True])
-def test_bound_fails_everywhere(gpu, combined):
+def test_bound_fails_everywhere(gpu, combined, prune):
     """Flat transitions and duplicated emission rows: the per-wave Viterbi's bound test
     (wave_tasks.h) fails for every target of every column, so every column runs all nine
     scan columns, and the exact ties must still resolve to the lowest state.  Hundreds of
     blocks under 2,048 columns, so the per-wave layout takes them (itr_viterbi and
-    itr_forward_viterbi)."""
+    itr_forward_viterbi), on either step."""
     import torch
 
     rng = np.random.default_rng(6)
@@ -102,6 +108,7 @@ def test_bound_fails_everywhere(gpu, combined):
     obs, off, _ = sample_alignment(a, b, pi, lengths, seed=11)
     t = build_tables(a, b, pi)
     model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    plan.set_prune_len(prune)
     d_obs = torch.from_numpy(obs.astype(np.int16)).to(gpu)
     if combined:
         ll, path = hmm.forward_viterbi_device(model, plan, d_obs)
@@ -112,11 +119,12 @@ def test_bound_fails_everywhere(gpu, combined):
     np.testing.assert_array_equal(path.cpu().numpy(), O.viterbi(t, obs, off))
 
 
+@pytest.mark.parametrize("prune", PRUNE)
 @pytest.mark.parametrize("n", [65, 70, 72])
-def test_viterbi_zero_probabilities(gpu, n):
+def test_viterbi_zero_probabilities(gpu, n, prune):
     """Zeros in a, b and pi (log 0 = -inf in the Viterbi's sums): unreachable states,
     impossible emissions and targets without any off-diagonal source, at the state counts of
-    the per-wave layout."""
+    the per-wave layout, on either step."""
     rng = np.random.default_rng(90 + n)
     a, b, pi = random_hmm(rng, n, stay=(0.5, 0.99))
     a[rng.random((n, n)) < 0.5] = 0.0
@@ -133,6 +141,7 @@ def test_viterbi_zero_probabilities(gpu, n):
     obs, off, _ = sample_alignment(a, b, pi, lengths, seed=n, p_n=0.02, p_gap=0.01)
     t = build_tables(a, b, pi)
     model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    plan.set_prune_len(prune)
     np.testing.assert_array_equal(hmm._paths(model, plan, obs), O.viterbi(t, obs, off))
 
 

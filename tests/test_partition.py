@@ -19,11 +19,11 @@ CUS = 256  # MI355X
 def info(lengths, cus=CUS):
     off = np.zeros(len(lengths) + 1, np.int64)
     off[1:] = np.cumsum(lengths)
-    out = np.zeros(8, np.int64)
+    out = np.zeros(10, np.int64)
     _lib.check(_lib.lib().itr_plan_partition_info(_lib.ptr(off), len(lengths), cus,
                                                   _lib.ptr(out)))
     keys = ("vit_nlong", "vit_long_cols", "vit_reserve", "fwd_reserve", "wave_ok",
-            "vit_nlong_v", "fwd_valu_tasks", "mix_entries")
+            "vit_nlong_v", "fwd_valu_tasks", "mix_entries", "prune_len", "prune_len_v")
     return dict(zip(keys, out.tolist()))
 
 
@@ -98,8 +98,25 @@ def test_cu_count_scales(lib):
     assert info(lengths, 128)["vit_nlong"] <= info(lengths, 256)["vit_nlong"]
 
 
+def test_prune_lengths(lib):
+    """The per-wave Viterbi's bound-pruned step takes the blocks shorter than the expected
+    makespan / kPruneCol (1.4 us): chr10's bulk blocks below ~5 kbp (the full scan for the
+    longer ones, whose step latency sets the makespan), every block of chr100 on one GPU
+    (throughput-bound), ~6.3 kbp in each world-8 shard."""
+    d = info(geometric(10_000_000))
+    assert 4500 <= d["prune_len"] <= 5500 and 3500 <= d["prune_len_v"] <= 4700
+    lengths = geometric(100_000_000)
+    assert info(lengths)["prune_len"] > lengths.max()
+    for lo, hi in shard_ranges(lengths, 8):
+        assert 5500 <= info(lengths[lo:hi])["prune_len"] <= 7000
+
+
+def test_set_prune_len_rejects_null(lib):
+    assert lib.itr_plan_set_prune_len(None, 0) != 0
+
+
 def test_bad_arguments(lib):
-    out = np.zeros(8, np.int64)
+    out = np.zeros(10, np.int64)
     off = np.array([0, 10], np.int64)
     assert lib.itr_plan_partition_info(_lib.ptr(off), 1, 0, _lib.ptr(out)) == _lib.ITR_EINVAL
     bad = np.array([0, 10, 5], np.int64)
