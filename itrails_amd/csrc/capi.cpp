@@ -1449,26 +1449,57 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     af.sK = p->d_sK;
     // (the forward's reserved set exists without the forward too — one partition, one set
     // of streams per plan; the Viterbi-only call sweeps its long set on it too)
-    if (split_fwd) {
-      HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
-      HIP_TRY(hipMemsetAsync(p->d_queue + 8, 0, 2 * sizeof(int), st));  // the idle loops' counters
+    // every work counter of this call, [2] .. [13], in one memset before the fork (the bulk
+    // queue is shared with the reserved CUs' late launches)
+    HIP_TRY(hipMemsetAsync(p->d_queue + 2, 0, 12 * sizeof(int), st));
+    hipStream_t sb = st;
+    int ocus = cus - reserve_cus;  // CUs of the sb launches
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_MIX_CUS")) ocus = atoi(getenv("ITR_MIX_CUS"));
+#endif
+    // the mixed launch: forward groups (the hybrid plan's matrix-core tasks) and the per-wave
+    // Viterbi blocks from one queue ordered by expected duration (plan: mix list)
+    itr::WaveMfmaArgs f{};
+    if (mixed) {
+      f.n = m->n;
+      f.ngroups = p->ngroups_ll;
+      f.groups = p->d_groups_ll;
+      f.tasks = p->d_mtasks;
+      f.off = p->d_off;
+      f.obs = obs;
+      f.a = m->a;
+      f.aT = m->aT;
+      f.ef = m->EF;
+      f.emit = m->E;
+      f.init = m->PIE;
+      f.loglik = fwd_loglik;
+      f.svec = p->d_svec;
+      f.sstride = gf.xr;
+      f.sK = p->d_sK;
+      f.prio_len = p->mix_prio_fwd;
+      w.prio_len = p->mix_prio_vit;
     }
-    // before the fork: the bulk queue is shared with the reserved CUs' late launch
-    HIP_TRY(hipMemsetAsync(mixed ? p->d_queue + 12 : w.queue, 0, sizeof(int), st));
-    if (nlong > 0) HIP_TRY(hipMemsetAsync(p->d_queue + 13, 0, sizeof(int), st));
-    if (nlong > 0 && vonly) HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
+    auto launch_bulk = [&]() -> int {  // (the makespan's critical path: enqueued first)
+      const int64_t grid = std::min<int64_t>((int64_t)wf.mixed_per_cu * ocus, (p->nmix + 3) / 4);
+      HIP_TRY(itr::launch_wave_mixed(wf, (int)grid, w, f, p->d_mix, (int)p->nmix,
+                                     p->d_queue + 12, sb));
+      return 0;
+    };
     if (reserve_cus > 0) {
       // the long blocks' Viterbi on lng (rvr CUs), the forward's VALU halves on lng2 (rfr
       // others): separate masks, so each set joins the bulk queue as soon as its own long
       // work is done without a bulk workgroup landing beside a running long task
       if (int e = partition(rvr, rfr, &pt)) return e;
       HIP_TRY(hipEventRecord(pt->fork, st));
-      HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
       HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
+      HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
       HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
+      sb = pt->blk;
+      if (mixed)
+        if (int e = launch_bulk()) return e;
       if (nlong > 0 && !vonly) {
         a.nblocks = nlong;
-        if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, rvr)) return e;
+        if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, rvr, 0, false)) return e;
         itr::TraceArgs tl = trace_args();
         tl.nblocks = nlong;
         tl.order = p->d_order;
@@ -1488,36 +1519,10 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
                                rfr, false))
           return e;
       }
+    } else if (mixed) {
+      if (int e = launch_bulk()) return e;
     }
-    hipStream_t sb = pt ? pt->blk : st;
-    int ocus = cus - reserve_cus;  // CUs of the sb launches
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_MIX_CUS")) ocus = atoi(getenv("ITR_MIX_CUS"));
-#endif
     if (mixed) {
-      // forward groups (the hybrid plan's matrix-core tasks) and the per-wave Viterbi blocks
-      // from one queue ordered by expected duration (plan: mix list)
-      itr::WaveMfmaArgs f{};
-      f.n = m->n;
-      f.ngroups = p->ngroups_ll;
-      f.groups = p->d_groups_ll;
-      f.tasks = p->d_mtasks;
-      f.off = p->d_off;
-      f.obs = obs;
-      f.a = m->a;
-      f.aT = m->aT;
-      f.ef = m->EF;
-      f.emit = m->E;
-      f.init = m->PIE;
-      f.loglik = fwd_loglik;
-      f.svec = p->d_svec;
-      f.sstride = gf.xr;
-      f.sK = p->d_sK;
-      f.prio_len = p->mix_prio_fwd;
-      w.prio_len = p->mix_prio_vit;
-      const int64_t grid = std::min<int64_t>((int64_t)wf.mixed_per_cu * ocus, (p->nmix + 3) / 4);
-      HIP_TRY(itr::launch_wave_mixed(wf, (int)grid, w, f, p->d_mix, (int)p->nmix,
-                                     p->d_queue + 12, sb));
       if (pt) {  // the reserved CUs join the bulk queue when their long work is done
         if (rvr > 0)
           HIP_TRY(itr::launch_wave_mixed(wf, wf.mixed_per_cu * rvr, w, f, p->d_mix,
