@@ -308,8 +308,10 @@ def oracle_check_post(a, b, pi, obs, off, post_dev_rows, nb, threads):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    # (defaults: 10 untimed steps bring the GPU to its steady clock first — with 2, the
+    # first timed steps ran 2-9 % slower than the calls' own event timers; 20 timed steps)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", choices=["auto", "chr10", "chr100"], default="auto")
     ap.add_argument("--n-int", type=int, default=5)
     ap.add_argument("--mode", choices=["fv", "vit", "posterior", "optimize"], default="fv",

@@ -306,6 +306,7 @@ struct itr_plan {
   // CU partition (plan_partition): reserved CUs for the long blocks' Viterbi and for the
   // forward's VALU halves; wave_ok = false when the long work cannot fit half the chip
   int vit_reserve = 0, fwd_reserve = 0;
+  int long_per_cu = 1;  // long Viterbi blocks a reserved CU sweeps at a time
   bool wave_ok = true;
   int32_t* d_mix = nullptr;
   int mix_prio_fwd = INT32_MAX, mix_prio_vit = INT32_MAX;
@@ -371,6 +372,15 @@ int vit_stride(int n) {
 //               load at N = 70 of a matrix-core forward group (~0.92 us) and a per-wave Viterbi
 //               block (~0.64 us), measured on chr10 (profiles/r3l_*)
 //   kMixPrio    mixed-queue entries that run at raised wave priority: about one per SIMD pair
+//   kVitPair    a 9-wave Viterbi block's step with a second long block on its CU (k x 8 blocks
+//               of 18,377 columns on 8 CUs: 318 / 407 / 613 ns per column for k = 1 / 2 / 3,
+//               profiles/r4pp_pair_long_blocks.txt)
+//   kPairSlack  the long set is swept two blocks per CU when its longest block at kVitPair
+//               fits within kPairSlack x the expected makespan (the forward+Viterbi call's
+//               makespan runs ~7 % over T on chr10: 7.5 vs 7.03 ms): chr10 7.65-7.72 ->
+//               7.41-7.52 ms per step with the long set on 32 instead of 40 CUs; the chr100
+//               shards keep one block per CU where packing two shorter blocks in sequence on a
+//               paired CU would overrun (same box, r4pp)
 //   kPruneCol   a per-wave Viterbi block takes the bound-pruned step (fewer instructions per
 //               column, a longer dependent chain: wave_tasks.h) when its length x kPruneCol
 //               fits within the expected makespan, the full scan otherwise; chr10
@@ -389,6 +399,7 @@ int vit_stride(int n) {
 constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kBulkCu = 180e-9, kFwdValu = 370e-9,
                  kBulkVit = 115e-9, kVitWaveLatV = 700e-9, kMixFwd = 0.92, kMixVit = 0.64,
                  kMixGroupCol = 1.4e-6, kPruneCol = 1.4e-6;
+constexpr double kVitPair = 407e-9, kPairSlack = 1.07;
 constexpr int64_t kMixPrio = 512;
 
 // Bins of capacity `cap` (first fit, items longest first): the CUs a set of sequential tasks
@@ -432,7 +443,18 @@ void plan_partition(itr_plan_t p, const std::vector<int64_t>& ulen, int cus) {
   }
   p->vit_nlong = k;
   p->vit_long_cols = cols;
-  const int rv = ffd_bins(lng, T / kVitLone);
+  // two long blocks per reserved CU at a time when the longest still fits the makespan at the
+  // paired step time: about half the reserved CUs for the same long work
+  double pair = kVitPair;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_VIT_PAIR")) pair = atof(getenv("ITR_VIT_PAIR"));
+#endif
+  int lpc = tmax * pair <= kPairSlack * T ? 2 : 1;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_LONG_PER_CU")) lpc = std::max(1, atoi(getenv("ITR_LONG_PER_CU")));
+#endif
+  p->long_per_cu = lpc;
+  const int rv = (ffd_bins(lng, T / (lpc > 1 ? pair : kVitLone)) + lpc - 1) / lpc;
   std::vector<int64_t> halves(ulen);
   std::sort(halves.begin(), halves.end(), std::greater<int64_t>());
   const int rf = ffd_bins(halves, T / kFwdValu);
@@ -529,7 +551,7 @@ uint64_t* g_diag = nullptr;  // diagnostic build: per-segment cycle sums of the 
 // tname: kernel timer (nullptr: none); max_grid > 0 caps the persistent grid
 // cus: the CUs the launch's stream may use (default: all)
 int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
-              int64_t max_grid = -1, int cus = 0, bool zero_queue = true) {
+              int64_t max_grid = -1, int cus = 0, bool zero_queue = true, bool share_cu = false) {
   itr::SweepGeometry g = itr::sweep_geometry(a.n, mode);
   if (g.iq < 0) return fail(ITR_EINVAL, "n_states=%d unsupported", a.n);
   a.xp = g.xp;
@@ -538,7 +560,8 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
   if (grid > a.nblocks) grid = a.nblocks;
   if (max_grid > 0 && grid > max_grid) grid = max_grid;
   if (grid <= 0) return 0;
-  if (grid <= cus) g.lds = std::max(g.lds, itr::kExclusiveLds);  // one per CU
+  // one per CU (unless the caller packs several long blocks per CU: share_cu)
+  if (grid <= cus && !share_cu) g.lds = std::max(g.lds, itr::kExclusiveLds);
   if (zero_queue) HIP_TRY(hipMemsetAsync(a.queue, 0, sizeof(int), st));
 #ifdef ITR_DIAG
   if (getenv("ITR_VERBOSE"))
@@ -1499,7 +1522,10 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
         if (int e = launch_bulk()) return e;
       if (nlong > 0 && !vonly) {
         a.nblocks = nlong;
-        if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, rvr, 0, false)) return e;
+        const int lpc = p->long_per_cu;
+        if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, (int64_t)lpc * rvr, 0, false,
+                              lpc > 1))
+          return e;
         itr::TraceArgs tl = trace_args();
         tl.nblocks = nlong;
         tl.order = p->d_order;
@@ -1509,10 +1535,15 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
         traced = nlong;
       } else if (nlong > 0) {  // Viterbi alone: both reserved sets sweep the long set
         a.nblocks = nlong;
+        const int lpc = p->long_per_cu;
         if (rvr > 0)
-          if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, rvr, 0, false)) return e;
+          if (int e = run_sweep(itr::MODE_VIT, a, pt->lng, nullptr, (int64_t)lpc * rvr, 0, false,
+                                lpc > 1))
+            return e;
         if (rfr > 0)
-          if (int e = run_sweep(itr::MODE_VIT, a, pt->lng2, nullptr, rfr, 0, false)) return e;
+          if (int e = run_sweep(itr::MODE_VIT, a, pt->lng2, nullptr, (int64_t)lpc * rfr, 0, false,
+                                lpc > 1))
+            return e;
       }
       if (split_fwd) {
         if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, pt->lng2, nullptr, true, false,
