@@ -372,15 +372,14 @@ int vit_stride(int n) {
 //               load at N = 70 of a matrix-core forward group (~0.92 us) and a per-wave Viterbi
 //               block (~0.64 us), measured on chr10 (profiles/r3l_*)
 //   kMixPrio    mixed-queue entries that run at raised wave priority: about one per SIMD pair
-//   kVitPair    a 9-wave Viterbi block's step with a second long block on its CU (k x 8 blocks
-//               of 18,377 columns on 8 CUs: 318 / 407 / 613 ns per column for k = 1 / 2 / 3,
-//               profiles/r4pp_pair_long_blocks.txt)
-//   kPairSlack  the long set is swept two blocks per CU when its longest block at kVitPair
-//               fits within kPairSlack x the expected makespan (the forward+Viterbi call's
-//               makespan runs ~7 % over T on chr10: 7.5 vs 7.03 ms): chr10 7.65-7.72 ->
-//               7.41-7.52 ms per step with the long set on 32 instead of 40 CUs; the chr100
-//               shards keep one block per CU where packing two shorter blocks in sequence on a
-//               paired CU would overrun (same box, r4pp)
+//   kVitPairEff the effective step of a 9-wave Viterbi block that shares its reserved CU with a
+//               second long block for part of its sweep (alone 318 ns, with a partner for the
+//               whole sweep 407 ns, three per CU 613 ns; profiles/r4pp_pair_long_blocks.txt);
+//   kPairShare  two long blocks per reserved CU only when the one-per-CU long set would hold
+//               more than this share of the chip: chr10 (35 CUs) 7.62-7.70 -> 7.44-7.48 ms
+//               per step with the long set on 24 CUs (same box, interleaved); the chr100
+//               shards (12-16 CUs) keep one per CU: paired with bins sized by 360 ns, one
+//               shard went 8.5 -> 9.5 ms (profiles/r4pab_pair_ab.txt)
 //   kPruneCol   a per-wave Viterbi block takes the bound-pruned step (fewer instructions per
 //               column, a longer dependent chain: wave_tasks.h) when its length x kPruneCol
 //               fits within the expected makespan, the full scan otherwise; chr10
@@ -398,8 +397,8 @@ int vit_stride(int n) {
 // benchmark layouts, so that a recalibration cannot move a layout onto another branch unseen.
 constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kBulkCu = 180e-9, kFwdValu = 370e-9,
                  kBulkVit = 115e-9, kVitWaveLatV = 700e-9, kMixFwd = 0.92, kMixVit = 0.64,
-                 kMixGroupCol = 1.4e-6, kPruneCol = 1.4e-6;
-constexpr double kVitPair = 407e-9, kPairSlack = 1.07;
+                 kMixGroupCol = 1.4e-6, kPruneCol = 1.4e-6, kVitPairEff = 360e-9,
+                 kPairShare = 1.0 / 8;
 constexpr int64_t kMixPrio = 512;
 
 // Bins of capacity `cap` (first fit, items longest first): the CUs a set of sequential tasks
@@ -443,18 +442,24 @@ void plan_partition(itr_plan_t p, const std::vector<int64_t>& ulen, int cus) {
   }
   p->vit_nlong = k;
   p->vit_long_cols = cols;
-  // two long blocks per reserved CU at a time when the longest still fits the makespan at the
-  // paired step time: about half the reserved CUs for the same long work
-  double pair = kVitPair;
+  // Long blocks a reserved CU sweeps at a time: two (bins sized by the shared step
+  // kVitPairEff) when the one-per-CU long set would hold more than kPairShare of the chip
+  // and its longest block still fits the makespan at the shared step — the freed CUs go to
+  // the bulk; otherwise one.
+  double step = kVitLone, pstep = kVitPairEff;
 #ifdef ITR_EXPERIMENT
-  if (getenv("ITR_VIT_PAIR")) pair = atof(getenv("ITR_VIT_PAIR"));
+  if (getenv("ITR_VIT_PAIR")) pstep = atof(getenv("ITR_VIT_PAIR"));
 #endif
-  int lpc = tmax * pair <= kPairSlack * T ? 2 : 1;
+  int lpc = 1;
+  if (ffd_bins(lng, T / kVitLone) > kPairShare * cus && tmax * pstep <= T) {
+    lpc = 2;
+    step = pstep;
+  }
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_LONG_PER_CU")) lpc = std::max(1, atoi(getenv("ITR_LONG_PER_CU")));
 #endif
   p->long_per_cu = lpc;
-  const int rv = (ffd_bins(lng, T / (lpc > 1 ? pair : kVitLone)) + lpc - 1) / lpc;
+  const int rv = (ffd_bins(lng, T / step) + lpc - 1) / lpc;
   std::vector<int64_t> halves(ulen);
   std::sort(halves.begin(), halves.end(), std::greater<int64_t>());
   const int rf = ffd_bins(halves, T / kFwdValu);

@@ -41,13 +41,13 @@ def lib():
 
 
 def test_chr10(lib):
-    """BASELINE config 2 (bench default): 59 long blocks on 30 reserved CUs, two at a time per
-    CU (kVitPair: the longest at the paired step fits the makespan), + 20 CUs for the
+    """BASELINE config 2 (bench default): 59 long blocks, two at a time per reserved CU on 21
+    CUs (one per CU they would need 35: more than 1/8 of the chip), + 20 CUs for the
     forward's VALU halves in the forward+Viterbi call, 69 long blocks in the Viterbi-only call
     (profiles/r4m_vit_long_set.txt: 59..80 long blocks all within 1 % of the best)."""
     d = info(geometric(10_000_000))
     assert d["wave_ok"] == 1
-    assert d["vit_nlong"] == 59 and d["vit_reserve"] == 30 and d["fwd_reserve"] == 20
+    assert d["vit_nlong"] == 59 and d["vit_reserve"] == 21 and d["fwd_reserve"] == 20
     assert d["vit_nlong_v"] == 69
     assert 40 <= d["vit_nlong"] <= 80 and 59 <= d["vit_nlong_v"] <= 80
 
@@ -72,6 +72,8 @@ def test_chr100_world8_shard(lib, rank):
     assert d["wave_ok"] == 1
     assert 20 <= d["vit_nlong"] <= 30
     assert d["vit_reserve"] + d["fwd_reserve"] <= CUS // 2
+    # one long block per reserved CU: the one-per-CU long set is under 1/8 of the chip
+    assert d["vit_reserve"] <= CUS // 8
     # the makespan floor of the VALU-task threshold (kMixGroupCol): 6-12 forward CUs, not 20-34
     assert 1 <= d["fwd_reserve"] <= 12
     assert d["vit_nlong_v"] >= d["vit_nlong"]
