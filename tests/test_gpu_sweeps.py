@@ -119,6 +119,27 @@ def test_bound_fails_everywhere(gpu, combined, prune):
     np.testing.assert_array_equal(path.cpu().numpy(), O.viterbi(t, obs, off))
 
 
+def test_paired_long_set_vs_oracle(gpu):
+    """The long Viterbi set swept two blocks per reserved CU (40 blocks of 3,000 columns beside
+    2 M columns of short blocks: tests/test_partition.py test_long_set_pairing), through
+    itr_forward_viterbi and itr_viterbi, every block against the CPU restatement."""
+    import torch
+
+    rng = np.random.default_rng(5)
+    lengths = [3000] * 40 + list(rng.integers(100, 600, size=5600))
+    g = golden("model_kat_5_5.npz")
+    a, b, pi = g["a"], g["b"], g["pi"]
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=21)
+    t = build_tables(a, b, pi)
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).to(gpu)
+    ref = O.viterbi(t, obs, off)
+    ll, path = hmm.forward_viterbi_device(model, plan, d_obs)
+    np.testing.assert_array_equal(path.cpu().numpy(), ref)
+    np.testing.assert_allclose(ll.cpu().numpy(), O.forward_loglik(t, obs, off), rtol=RTOL, atol=0)
+    np.testing.assert_array_equal(hmm.viterbi_device(model, plan, d_obs).cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("prune", PRUNE)
 @pytest.mark.parametrize("n", [65, 70, 72])
 def test_viterbi_zero_probabilities(gpu, n, prune):

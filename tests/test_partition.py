@@ -101,6 +101,20 @@ def test_cu_count_scales(lib):
     assert info(lengths, 128)["vit_nlong"] <= info(lengths, 256)["vit_nlong"]
 
 
+def _paired_layout(n_short):
+    rng = np.random.default_rng(5)
+    return [3000] * 40 + list(rng.integers(100, 600, size=n_short))
+
+
+def test_long_set_pairing(lib):
+    """Two long blocks per reserved CU only when one per CU would take more than 1/8 of the
+    chip and the longest fits the makespan at the shared step (capi.cpp kVitPairEff,
+    kPairShare): 40 blocks of 3,000 columns beside 2 M columns of short blocks -> 20 CUs;
+    the same 40 beside 0.2 M columns (makespan = the longest block's lone sweep) -> 40."""
+    assert info(_paired_layout(5600))["vit_reserve"] == 20
+    assert info(_paired_layout(600))["vit_reserve"] == 40
+
+
 def test_prune_lengths(lib):
     """The per-wave Viterbi's bound-pruned step takes the blocks shorter than the expected
     makespan / kPruneCol (1.4 us): chr10's bulk blocks below ~5 kbp (the full scan for the
