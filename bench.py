@@ -196,16 +196,28 @@ def pmc_traffic(n, mode, tag_hint=""):
     return None, "no PMC summary under profiles/ for this kernel"
 
 
+def lib_sha256():
+    import hashlib
+    from itrails_amd import _lib
+    return hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
+
+
 def fv_call_traffic():
     """HBM bytes per itr_forward_viterbi call (every launch of the call) from the newest
     committed profiles/r*_fv_call_traffic.json (scripts/fv_traffic.py over the FETCH_SIZE /
-    WRITE_SIZE passes of the default bench command, scripts/r4/final.sh)."""
+    WRITE_SIZE passes of the default bench command), only when that profile ran the library
+    this run loads (library_sha256): a kernel change makes the old bytes stale, and then the
+    line carries null with the old file named."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fv_call_traffic.json")))
     if not files:
         return None, "no per-call PMC traffic under profiles/"
     d = json.load(open(files[-1]))
-    return d["bytes_per_call"], (f"{os.path.basename(files[-1])}: FETCH_SIZE+WRITE_SIZE of every "
-                                 f"launch of the call ({len(d['per_kernel'])} kernels), raw")
+    name = os.path.basename(files[-1])
+    if d.get("library_sha256") != lib_sha256():
+        return None, (f"{name} was profiled on another build of the library (not this one): "
+                      "no traffic for this build")
+    return d["bytes_per_call"], (f"{name}: 2 x FETCH_SIZE + WRITE_SIZE of every launch of the "
+                                 f"call ({len(d['per_kernel'])} kernels), this build")
 
 
 def pmc_rates(n):
@@ -288,20 +300,30 @@ def oracle_time(a, b, pi, obs, off, sample_cols, threads, posterior):
     return int(o2[-1]), time.perf_counter() - t0
 
 
-def oracle_check_post(a, b, pi, obs, off, post_dev_rows, nb, threads):
+def oracle_check_post(a, b, pi, obs, off, d_post, threads, chunk_cols=1_000_000):
+    """Every posterior row of this rank against the CPU restatement, in runs of whole blocks
+    of ~chunk_cols columns (10 Mbp x 133 states is 10.6 GB of rows): allclose at 1e-8, the
+    largest relative error over rows > 1e-200, and the restatement's own time (the all-cores
+    CPU baseline of posterior mode)."""
     from itrails_amd.tables import build_tables
     from oracle import hmm_oracle as O
 
     O.set_threads(threads)
     t = build_tables(a, b, pi)
-    o2 = off[: nb + 1]
-    t0 = time.perf_counter()
-    ref = O.posterior(t, obs[: o2[-1]], o2)
-    dt = time.perf_counter() - t0
-    ok = bool(np.allclose(post_dev_rows, ref, rtol=1e-8, atol=1e-300))
-    big = ref > 1e-200
-    rel = float(np.max(np.abs(post_dev_rows[big] - ref[big]) / ref[big])) if big.any() else 0.0
-    return dict(ok=ok, max_rel=rel, cols=int(o2[-1]), seconds=dt)
+    nb = len(off) - 1
+    k0, ok, rel, dt = 0, True, 0.0, 0.0
+    while k0 < nb:
+        k1 = min(nb, max(k0 + 1, int(np.searchsorted(off, off[k0] + chunk_cols, side="right")) - 1))
+        t0 = time.perf_counter()
+        ref = O.posterior(t, obs[off[k0]:off[k1]], off[k0:k1 + 1] - off[k0])
+        dt += time.perf_counter() - t0
+        rows = d_post[int(off[k0]):int(off[k1])].cpu().numpy()
+        ok = ok and bool(np.allclose(rows, ref, rtol=1e-8, atol=1e-300))
+        big = ref > 1e-200
+        if big.any():
+            rel = max(rel, float(np.max(np.abs(rows[big] - ref[big]) / ref[big])))
+        k0 = k1
+    return dict(ok=ok, max_rel=rel, cols=int(off[-1]), seconds=dt)
 
 
 # ---------------------------------------------------------------------------------------
@@ -351,9 +373,13 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the exchange with several ranks on one GPU)")
+    ap.add_argument("--dist", type=int, default=0, choices=[0, 1],
+                    help="1: initialise the process group even at N = 1, so every step's "
+                         "log-likelihood exchange is a real collective (RCCL with --backend "
+                         "nccl) beside the CU-masked sweep streams")
     args = ap.parse_args()
 
-    if args.gpus > 1:
+    if args.gpus > 1 or args.dist:
         # RCCL's own streams beside the launch stream and the three CU-masked streams of
         # itr_forward_viterbi exceed the 4 hardware queues a process gets by default; shared
         # queues serialise.  Set before HIP starts (ranks inherit it).
@@ -374,16 +400,21 @@ def main():
     dev = torch.device("cuda", local)
     if args.stream == "side":  # every launch of this process on one created stream
         torch.cuda.set_stream(torch.cuda.Stream(device=dev))
-    if world > 1:
+    dist_on = world > 1 or args.dist == 1
+    if dist_on:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
     cdev = dev if args.backend == "nccl" else torch.device("cpu")  # collective tensors
-    seen_world = dist.get_world_size() if world > 1 else 1
+    seen_world = dist.get_world_size() if dist_on else 1
 
     def allreduce(x, op="sum"):
-        if world == 1:
+        if not dist_on:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
@@ -421,7 +452,7 @@ def main():
         # exact gather (x + 0 = x); the block-order host sum happens after the timed region
         d_ll_global.zero_()
         d_ll_global[lo:lo + plan.nblocks] = d_ll.to(cdev)
-        if world > 1:
+        if dist_on:
             dist.all_reduce(d_ll_global)
 
     def opt_step(timing=False, xchg=True):
@@ -499,17 +530,25 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
+    # the timed call's own HIP-event duration (fork to join, on its stream), read after every
+    # timed step (each fv / vit step ends synchronised, so the read adds no wait): the
+    # roofline's kernel_ms comes from the same loop as ms_per_step
+    loop_ms = []
+    loop_timer = {"fv": "forward_viterbi", "vit": "viterbi"}.get(args.mode) \
+        if args.overlap else None
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+        if loop_timer:
+            loop_ms.append(hmm.last_kernel_ms(loop_timer))
         if os.environ.get("BENCH_STEP_TIMES"):  # diagnostics only: per-step wall times
             torch.cuda.synchronize()
             print(f"step {(time.perf_counter() - t0) * 1e3:.3f} ms", file=sys.stderr)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     dt = allreduce(time.perf_counter() - t0, "max")
@@ -520,7 +559,7 @@ def main():
     # N > 1: each rank's own step time without the exchange (its share of the work; the
     # timed step waits for the slowest rank inside the all-reduce) and the exchange alone
     per_rank_ms, xchg_ms = None, None
-    if world > 1:
+    if dist_on:
         own = []
         for _ in range(max(1, min(args.steps, 3))):
             torch.cuda.synchronize()
@@ -564,9 +603,7 @@ def main():
                  "reference": "oracle/hmm_oracle.c (CPU restatement of optimizer.py:145-354, "
                               "pinned to the reference's golden vectors)"}
     elif args.verify and post_mode:
-        nb = max(1, int(np.searchsorted(off, 1_000_000)))
-        rows = d_post[: int(off[nb])].cpu().numpy()
-        c = oracle_check_post(a, b, pi, obs, off, rows, nb, threads)
+        c = oracle_check_post(a, b, pi, obs, off, d_post, threads)
         sums = float((d_post.sum(dim=1) - 1.0).abs().max())
         check = {"posterior_allclose_1e-8": bool(allreduce(1.0 if c["ok"] else 0.0, "min")),
                  "posterior_max_rel_err": allreduce(c["max_rel"], "max"),
@@ -627,13 +664,14 @@ def main():
             dom = ("itr_forward_viterbi: hybrid_sweep_kernel<FWD_LL> (forward VALU halves, "
                    "reserved CUs) | sweep_kernel<VIT> (longest blocks, reserved CUs) | "
                    "wave_mixed_kernel (forward groups + per-wave Viterbi, the rest)")
-            dom_ms = fv_avg if fv_avg else vit_avg
+            dom_ms = float(np.mean(loop_ms)) if loop_ms else (fv_avg if fv_avg else vit_avg)
             dom_peak = 2 * pair_ops * cols_local / (ideal_ms * 1e-3) / 1e12  # combined peak
             dom_mode = 3
         elif vit_mode:
             dom, dom_ms, dom_peak, dom_mode = ("Viterbi max-plus sweep: sweep_kernel<VIT> (longest "
                                                "blocks, both reserved CU sets) | wave_vit_kernel "
-                                               "(rest)"), vit_avg, am_peak, 3
+                                               "(rest)"), \
+                float(np.mean(loop_ms)) if loop_ms else vit_avg, am_peak, 3
             ideal_ms = pair_ops * cols_local / (am_peak * 1e12) * 1e3
         elif post_mode:
             dom, dom_ms, dom_peak, dom_mode = "sweep_kernel<BWD> (backward + posterior)", vit_avg, \
@@ -718,7 +756,7 @@ def main():
                        "longest_block_rank0": int(np.diff(off).max()) if plan.nblocks else 0,
                        "parallelism": f"block-sharded x{world}",
                        "world_size_seen": seen_world,
-                       "backend": (dist.get_backend() if world > 1 else None)},
+                       "backend": (dist.get_backend() if dist_on else None)},
             "roofline": {"kernel": dom, "bound": "valu",
                          "pipe": {"fv": "FP64 VALU (forward FMA + Viterbi add+max pairs)",
                                   "vit": "FP64 VALU (add+max pairs)"}.get(args.mode,
@@ -731,6 +769,9 @@ def main():
                          "peak_spec_tflops": FP64_SPEC_TFLOPS,
                          "traffic": traffic, "traffic_note": traffic_note,
                          "kernel_ms": round(dom_ms, 4),
+                         "kernel_ms_source": ("HIP events of the timed call in the timed loop "
+                                              f"({len(loop_ms)} steps)") if loop_ms else
+                                             "HIP events, separate instrumented passes",
                          "forward_ms": round(fwd_avg, 4),
                          "viterbi_ms": round(vit_avg, 4) if args.mode in ("fv", "vit") else None,
                          "traceback_ms": round(tb_avg, 4) if args.mode in ("fv", "vit") else None,
@@ -743,7 +784,7 @@ def main():
             **({"counters": {"source": rates_src, "kernels": rates}} if rates else {}),
             **({"build_ms": round(float(np.mean(build_ms)), 1)} if opt_mode else {}),
             **({"per_rank_step_ms": per_rank_ms, "allreduce_ms": xchg_ms,
-                "allreduce_bytes": int(d_ll_global.numel() * 8)} if world > 1 else {}),
+                "allreduce_bytes": int(d_ll_global.numel() * 8)} if dist_on else {}),
             # optimize mode with a split build: each rank's own step still contains the
             # build's all_gather, so it waits for the slowest rank's share of the build
             **({"per_rank_includes": "model build incl. its all_gather (split_build)"}
@@ -756,7 +797,7 @@ def main():
             "gen_seconds": round(gen_s, 2),
         }
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -71,6 +71,14 @@ ITR_API int itr_model_create(int n_states, const double* h_a, const double* h_lo
                              const double* h_pi_emit, const double* h_log_pi_emit,
                              itr_model_t* out);
 ITR_API int itr_model_destroy(itr_model_t model);
+/* Build the model's Viterbi slot tables now (the one-block-per-wavefront layout's padded and
+ * slot-ordered log-emission tables and per-slot bounds, N = 65..72 only; a no-op otherwise):
+ * a host simulation of 2,048 columns plus blocking allocations and copies, a few ms.  A model
+ * used for decoding should be prepared once after itr_model_create so that itr_viterbi /
+ * itr_forward_viterbi stay allocation-free and asynchronous on their stream; an unprepared
+ * model is prepared by its first Viterbi call, which then blocks the host for that time.  A
+ * model used only for likelihoods (the optimizer's per-evaluation models) never needs it. */
+ITR_API int itr_model_prepare_viterbi(itr_model_t model);
 ITR_API int itr_model_n_states(itr_model_t model, int* n);
 
 /* ---------------------------------------------------------------------------------- */
@@ -273,6 +281,15 @@ ITR_API int itr_chain_rows(int k, int n_groups, int rmax, const int32_t* d_src,
                            const int32_t* d_cols, const double* d_P, int64_t ldp,
                            const double* d_F, int64_t ldf, const double* d_M, double* d_out,
                            int64_t ldo, void* stream);
+
+/* Path-group sums of one rebuild's Van Loan integrals (run_markov_chain_ABC.py:478-486:
+ * the group's matrix S = S_0 + S_1 + ... over its paths, left to right):
+ * d_M[g] = d_S[d_paths[d_off[g]]] + d_S[d_paths[d_off[g] + 1]] + ... for g < n_groups, every
+ * matrix nn float64 values, each element summed in path order from 0.0 (bit-identical to
+ * the sequential sum).  d_off: n_groups + 1 int32 offsets into d_paths (int32 matrix indices
+ * of d_S); an empty group gives zeros. */
+ITR_API int itr_group_sum(int64_t nn, int n_groups, const int32_t* d_off,
+                          const int32_t* d_paths, const double* d_S, double* d_M, void* stream);
 
 /* ---------------------------------------------------------------------------------- */
 /* model build: emission rows                                                          */

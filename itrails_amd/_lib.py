@@ -32,6 +32,7 @@ _SIGNATURES = {
     "itr_device_count": ([ctypes.POINTER(_I)], _I),
     "itr_model_create": ([_I, _P, _P, _P, _P, _P, _P, ctypes.POINTER(_P)], _I),
     "itr_model_destroy": ([_P], _I),
+    "itr_model_prepare_viterbi": ([_P], _I),
     "itr_model_n_states": ([_P, ctypes.POINTER(_I)], _I),
     "itr_plan_create": ([_P, _I64, ctypes.POINTER(_P)], _I),
     "itr_plan_create_ex": ([_P, _I64, _D, _D, ctypes.POINTER(_P)], _I),
@@ -63,6 +64,7 @@ _SIGNATURES = {
     "itr_gemm_batched": ([_I, _I, _I, _I64, _D, _P, _P, _D, _P, _P], _I),
     "itr_chain_rows": ([_I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _P, _I64, _P, _P, _I64, _P],
                        _I),
+    "itr_group_sum": ([_I64, _I, _P, _P, _P, _P, _P], _I),
     "itr_emission_rows": ([_I, _P, _P, _P], _I),
     "itr_maf_open": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_char_p,
                       ctypes.POINTER(_P)], _I),
@@ -106,6 +108,8 @@ def lib():
     import torch  # noqa: F401
     L = ctypes.CDLL(LIB_PATH)
     for name, (args, res) in _SIGNATURES.items():
+        if os.environ.get("ITR_LIB") and not hasattr(L, name):
+            continue  # (an older library under A/B test: entry points it predates stay unbound)
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res

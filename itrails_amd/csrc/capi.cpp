@@ -125,9 +125,14 @@ struct Partitions {
       if (*q) {
         (void)hipStreamSynchronize(*q);
         (void)hipStreamDestroy(*q);
+        *q = nullptr;
       }
     for (hipEvent_t* e : {&x.fork, &x.jl, &x.jl2, &x.jb})
-      if (*e) (void)hipEventDestroy(*e);
+      if (*e) {
+        (void)hipEventDestroy(*e);
+        *e = nullptr;
+      }
+    x.device = -1;  // (matches no device: a slot whose re-creation failed stays unused)
     if (have_dev) (void)hipSetDevice(dev);
   }
   void release() {
@@ -210,13 +215,18 @@ int partition(int reserve, int reserve2, Partition** out, bool masked = true) {
   x.reserve = reserve;
   x.reserve2 = reserve2;
   x.masked = masked;
-  HIP_TRY(hipExtStreamCreateWithCUMask(&x.lng, (uint32_t)ml.size() * 32, ml.data()));
-  HIP_TRY(hipExtStreamCreateWithCUMask(&x.lng2, (uint32_t)ml2.size() * 32, ml2.data()));
-  HIP_TRY(hipExtStreamCreateWithCUMask(&x.blk, (uint32_t)mb.size() * 32, mb.data()));
-  HIP_TRY(hipEventCreateWithFlags(&x.fork, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&x.jl, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&x.jl2, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&x.jb, hipEventDisableTiming));
+  hipError_t err = hipExtStreamCreateWithCUMask(&x.lng, (uint32_t)ml.size() * 32, ml.data());
+  if (err == hipSuccess)
+    err = hipExtStreamCreateWithCUMask(&x.lng2, (uint32_t)ml2.size() * 32, ml2.data());
+  if (err == hipSuccess)
+    err = hipExtStreamCreateWithCUMask(&x.blk, (uint32_t)mb.size() * 32, mb.data());
+  for (hipEvent_t* e : {&x.fork, &x.jl, &x.jl2, &x.jb})
+    if (err == hipSuccess) err = hipEventCreateWithFlags(e, hipEventDisableTiming);
+  if (err != hipSuccess) {  // nothing half-built stays behind (the old slot is already dead)
+    Partitions::destroy(x);
+    return fail(ITR_EHIP, "partition: stream/event creation failed: %s", hipGetErrorString(err));
+  }
+  x.device = dev;
   x.mb = mb;
   if (slot) {
     *slot = x;  // (in place: the other devices' entries keep their addresses)
@@ -307,6 +317,7 @@ struct itr_plan {
   // forward's VALU halves; wave_ok = false when the long work cannot fit half the chip
   int vit_reserve = 0, fwd_reserve = 0;
   int long_per_cu = 1;  // long Viterbi blocks a reserved CU sweeps at a time
+  int fwd_per_cu = 1;   // forward VALU halves a reserved CU sweeps at a time
   bool wave_ok = true;
   int32_t* d_mix = nullptr;
   int mix_prio_fwd = INT32_MAX, mix_prio_vit = INT32_MAX;
@@ -398,7 +409,8 @@ int vit_stride(int n) {
 constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kBulkCu = 180e-9, kFwdValu = 370e-9,
                  kBulkVit = 115e-9, kVitWaveLatV = 700e-9, kMixFwd = 0.92, kMixVit = 0.64,
                  kMixGroupCol = 1.4e-6, kPruneCol = 1.4e-6, kVitPairEff = 360e-9,
-                 kPairShare = 1.0 / 8;
+                 kPairShare = 1.0 / 8, kFwdPairStep = 480e-9;
+constexpr int kFwdPairMin = 16;
 constexpr int64_t kMixPrio = 512;
 
 // Bins of capacity `cap` (first fit, items longest first): the CUs a set of sequential tasks
@@ -462,7 +474,24 @@ void plan_partition(itr_plan_t p, const std::vector<int64_t>& ulen, int cus) {
   const int rv = (ffd_bins(lng, T / step) + lpc - 1) / lpc;
   std::vector<int64_t> halves(ulen);
   std::sort(halves.begin(), halves.end(), std::greater<int64_t>());
-  const int rf = ffd_bins(halves, T / kFwdValu);
+  int rf = ffd_bins(halves, T / kFwdValu);
+  // two forward halves per reserved CU at a time when the one-per-CU set is large (more
+  // than kFwdPairMin CUs), bins sized by the shared step kFwdPairStep
+  int fpc = 1;
+  double fstep = kFwdPairStep;
+  int fmin = kFwdPairMin;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_FWD_PAIR_STEP")) fstep = atof(getenv("ITR_FWD_PAIR_STEP"));
+  if (getenv("ITR_FWD_PAIR_MIN")) fmin = atoi(getenv("ITR_FWD_PAIR_MIN"));
+#endif
+  if (rf > fmin) {
+    const int rf2 = (ffd_bins(halves, T / fstep) + 1) / 2;
+    if (rf2 < rf) {
+      rf = rf2;
+      fpc = 2;
+    }
+  }
+  p->fwd_per_cu = fpc;
   p->fwd_reserve = rf;  // (viterbi_impl rounds both up to whole XCC sets)
   p->vit_reserve = rv;
   p->wave_ok = rv + rf <= cus / 2;
@@ -593,7 +622,8 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
 // counters on `st` first (a split launch resets them once, before both parts).
 int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const itr::MfmaGeometry& g,
                hipStream_t st, const char* tname, bool valu = true, bool mfma = true,
-               int64_t max_grid = -1, bool zero_queues = true, int cus = 0) {
+               int64_t max_grid = -1, bool zero_queues = true, int cus = 0,
+               bool share_cu = false) {
   if (cus <= 0) cus = cu_count();
   itr::MfmaArgs a{};
   a.n = m->n;
@@ -644,7 +674,8 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   if (max_grid > 0) grid = std::min(grid, max_grid);
   if (grid <= 0) return 0;
   itr::MfmaGeometry gx = g;
-  if (grid <= cus) gx.lds_min = itr::kExclusiveLds;  // one workgroup per CU
+  // one workgroup per CU (unless the caller packs several VALU tasks per CU: share_cu)
+  if (grid <= cus && !share_cu) gx.lds_min = itr::kExclusiveLds;
   if (zero_queues) HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
 #ifdef ITR_DIAG
   if (getenv("ITR_VERBOSE"))
@@ -1551,8 +1582,12 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
             return e;
       }
       if (split_fwd) {
+        int64_t fg = (int64_t)p->fwd_per_cu * rfr;  // forward halves at a time on the set
+#ifdef ITR_EXPERIMENT
+        if (getenv("ITR_FWD_PER_CU")) fg = (int64_t)atoi(getenv("ITR_FWD_PER_CU")) * rfr;
+#endif
         if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, pt->lng2, nullptr, true, false,
-                               rfr, false))
+                               fg, false, 0, fg > rfr))
           return e;
       }
     } else if (mixed) {
@@ -1654,6 +1689,12 @@ int itr_block_rows(itr_model_t m, int kind, const uint16_t* obs, int64_t T, doub
   a.prev = kind == 2 ? prev : nullptr;
   HIP_TRY(itr::launch_rows(a, (hipStream_t)stream));
   return 0;
+}
+
+int itr_model_prepare_viterbi(itr_model_t m) {
+  if (int e = check_model(m)) return e;
+  if (m->xrw == 0) return 0;  // (no per-wave layout for this state count)
+  return vit_slot_tables(m);
 }
 
 int itr_backtrack_rows(const double* omega, const double* prev, int64_t T, int n, double* path,
@@ -2020,6 +2061,17 @@ int itr_chain_rows(int k, int ng, int rmax, const int32_t* src, const int32_t* o
   itr::ChainRowsArgs a{k, rmax, src, oms, ome, dst, cols, P, ldp, F, ldf, M, out, ldo};
   const hipError_t e = itr::chain_rows(a, ng, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ITR_EHIP, "chain rows failed: %s", hipGetErrorString(e));
+  return 0;
+}
+
+int itr_group_sum(int64_t nn, int ng, const int32_t* off, const int32_t* paths, const double* S,
+                  double* M, void* stream) {
+  if (nn < 1 || ng < 0 || ng > 65535)
+    return fail(ITR_EINVAL, "bad group-sum shape nn=%lld groups=%d", (long long)nn, ng);
+  if (ng == 0) return 0;
+  if (!off || !M) return fail(ITR_EINVAL, "null device pointer");
+  const hipError_t e = itr::group_sum(nn, ng, off, paths, S, M, (hipStream_t)stream);
+  if (e != hipSuccess) return fail(ITR_EHIP, "group sum failed: %s", hipGetErrorString(e));
   return 0;
 }
 

@@ -39,6 +39,8 @@ struct ChainRowsArgs {
   int64_t ldo;
 };
 hipError_t chain_rows(const ChainRowsArgs& a, int ngroups, hipStream_t st);
+hipError_t group_sum(int64_t nn, int ngroups, const int32_t* off, const int32_t* paths,
+                     const double* S, double* M, hipStream_t st);
 
 // Solve M X = R for every member (M n x n, R n x nrhs, both row-major, contiguous):
 // M is overwritten by its LU factors (partial pivoting), R by X.  `piv` is a device

@@ -242,6 +242,31 @@ __global__ void __launch_bounds__(256) chain_rows_kernel(ChainRowsArgs g) {
     }
 }
 
+// Path-group sums of the chain's Van Loan integrals: M[g] = S[p_g0] + S[p_g1] + ... for the
+// paths of group g in order, every element summed one after another from 0.0 — the
+// reference's left-to-right `S = S_0 + S_1 + ...` (run_markov_chain_ABC.py:478-486), one
+// launch for all groups instead of one indexed add per path position.
+__global__ void __launch_bounds__(256) group_sum_kernel(int64_t nn, const double* __restrict__ S,
+                                                        const int32_t* __restrict__ off,
+                                                        const int32_t* __restrict__ paths,
+                                                        double* __restrict__ M) {
+  const int g = blockIdx.y;
+  const int k0 = off[g], k1 = off[g + 1];
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nn; e += (int64_t)gridDim.x * 256) {
+    double acc = 0.0;
+    for (int k = k0; k < k1; ++k) acc += S[(int64_t)paths[k] * nn + e];
+    M[(int64_t)g * nn + e] = acc;
+  }
+}
+
+hipError_t group_sum(int64_t nn, int ngroups, const int32_t* off, const int32_t* paths,
+                     const double* S, double* M, hipStream_t st) {
+  if (ngroups <= 0 || nn <= 0) return hipSuccess;
+  const int gx = (int)std::min<int64_t>((nn + 255) / 256, 1024);
+  hipLaunchKernelGGL(group_sum_kernel, dim3(gx, ngroups), dim3(256), 0, st, nn, S, off, paths, M);
+  return hipGetLastError();
+}
+
 hipError_t chain_rows(const ChainRowsArgs& a, int ngroups, hipStream_t st) {
   if (ngroups <= 0 || a.rmax <= 0 || a.k <= 0) return hipSuccess;
   if (ngroups > 65535) return hipErrorInvalidValue;

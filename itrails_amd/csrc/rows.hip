@@ -112,7 +112,19 @@ __global__ void __launch_bounds__(64) backtrack_rows_kernel(const double* omega,
   path[T - 1] = (double)s;
   for (int64_t t = T - 2; t >= 0; --t) {
     const double b = prev[t * n + s];
+    // NumPy's prev[i, int(s)]: truncation, negative indices wrap once; anything else (NaN,
+    // +-inf, |s| >= n) is the reference's error: this and every earlier entry become NaN
+    // (the wrapper raises) and no out-of-range row is read
+    if (!(b > -(double)n - 1.0 && b < (double)n)) {
+      for (int64_t u = t; u >= 0; --u) path[u] = __builtin_nan("");
+      return;
+    }
     s = (int)b;
+    if (s < 0) s += n;
+    if (s < 0 || s >= n) {
+      for (int64_t u = t; u >= 0; --u) path[u] = __builtin_nan("");
+      return;
+    }
     path[t] = b;
   }
 }

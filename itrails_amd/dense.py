@@ -175,3 +175,16 @@ def chain_rows(P, F, M, tab, out, cols=None):
                                P.shape[1], p(F), F.shape[1] if F is not None else 0,
                                M.data_ptr(), out.data_ptr(), out.shape[1], _stream()))
     return out
+
+
+def group_sum(S, off, paths, ng, out=None):
+    """M[g] = S[paths[off[g]]] + S[paths[off[g] + 1]] + ... in path order (itr_group_sum);
+    off / paths: int32 device tensors."""
+    import torch
+    nn = S[0].numel() if S.shape[0] else int(np.prod(S.shape[1:]))
+    if out is None:
+        out = torch.empty((ng,) + tuple(S.shape[1:]), dtype=torch.float64, device=S.device)
+    if ng:
+        check(lib().itr_group_sum(nn, ng, off.data_ptr(), paths.data_ptr(),
+                                  S.data_ptr() if S.numel() else None, out.data_ptr(), _stream()))
+    return out

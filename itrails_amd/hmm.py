@@ -51,6 +51,12 @@ class Model:
         self.handle = h.value
         self.n = t.n
 
+    def prepare_viterbi(self):
+        """Build the Viterbi slot tables now (itr_model_prepare_viterbi), so that the decode
+        calls stay asynchronous; otherwise the first Viterbi call builds them."""
+        check(lib().itr_model_prepare_viterbi(self.handle))
+        return self
+
     def close(self):
         if getattr(self, "handle", None):
             lib().itr_model_destroy(self.handle)
@@ -379,4 +385,7 @@ def backtrack_viterbi(omega, prev) -> np.ndarray:
     d_path = torch.empty(T, dtype=torch.float64, device=d_om.device)
     check(lib().itr_backtrack_rows(ptr(d_om), ptr(d_prev) if d_prev is not None else None, T, n,
                                    ptr(d_path), _stream_handle()))
-    return d_path.cpu().numpy()
+    out = d_path.cpu().numpy()
+    if np.isnan(out).any():  # a back-pointer outside the states (the kernel stopped there)
+        raise IndexError(f"backtrack_viterbi: a back-pointer is not a state index in [-{n}, {n})")
+    return out

@@ -477,19 +477,34 @@ class _DevInterval:
     __slots__ = ("e_idx", "vl0", "vl1", "plain", "ng", "sum_steps", "rows", "rmax")
 
 
+class _GroupSums:
+    """The path groups of a set of group matrices M[g] = S[p_g0] + S[p_g1] + ...: as CSR
+    (int32 offsets + path indices, one itr_group_sum launch on the device) and as the
+    sequential steps of the same sums (step k adds the k-th path of every group that has
+    one) for a CPU-tensor rehearsal of the routing (tests)."""
+    __slots__ = ("ng", "off", "paths", "steps")
+
+
 def _group_tables(dev, pids_list, rows_of_group):
-    """Index tensors of a set of path groups: the sequential sum steps of each group's
-    matrix (step k adds the k-th path of every group that has one: the reference's
-    left-to-right S = S_0 + S_1 + ..., run_markov_chain_ABC.py:478-486) and, for the row
-    products, every row's (group, slot) in a zero-padded [groups, rmax] layout."""
+    """Index tensors of a set of path groups: the path sums of each group's matrix (the
+    reference's left-to-right S = S_0 + S_1 + ..., run_markov_chain_ABC.py:478-486) and, for
+    the row products, every row's (group, slot) in a zero-padded [groups, rmax] layout."""
     import torch
-    steps = []
-    kmax = max((len(p) for p in pids_list), default=0)
-    for k in range(kmax):
-        gs = [g for g, p in enumerate(pids_list) if len(p) > k]
-        ps = [int(pids_list[g][k]) for g in gs]
-        steps.append((torch.as_tensor(gs, dtype=torch.long, device=dev),
-                      torch.as_tensor(ps, dtype=torch.long, device=dev)))
+    gsum = _GroupSums()
+    gsum.ng = len(pids_list)
+    lens = [len(p) for p in pids_list]
+    gsum.off = torch.as_tensor(np.concatenate([[0], np.cumsum(lens)]).astype(np.int32),
+                               device=dev)
+    flat = [int(x) for p in pids_list for x in p]
+    gsum.paths = torch.as_tensor(np.asarray(flat, dtype=np.int32), device=dev)
+    gsum.steps = []
+    if torch.device(dev).type == "cpu":
+        kmax = max(lens, default=0)
+        for k in range(kmax):
+            gs = [g for g, p in enumerate(pids_list) if len(p) > k]
+            ps = [int(pids_list[g][k]) for g in gs]
+            gsum.steps.append((torch.as_tensor(gs, dtype=torch.long, device=dev),
+                               torch.as_tensor(ps, dtype=torch.long, device=dev)))
     gid, slot = [], []
     rmax = 0
     for g, rows in enumerate(rows_of_group):
@@ -497,8 +512,8 @@ def _group_tables(dev, pids_list, rows_of_group):
             gid.append(g)
             slot.append(k)
         rmax = max(rmax, rows)
-    return steps, (torch.as_tensor(gid, dtype=torch.long, device=dev),
-                   torch.as_tensor(slot, dtype=torch.long, device=dev)), rmax
+    return gsum, (torch.as_tensor(gid, dtype=torch.long, device=dev),
+                  torch.as_tensor(slot, dtype=torch.long, device=dev)), rmax
 
 
 def _device_tables(plan, Q, ss, la):
@@ -587,11 +602,18 @@ def _device_tables(plan, Q, ss, la):
     return tab
 
 
-def _group_matrices(S, steps, ng, n):
-    """M[g] = S[p_g0] + S[p_g1] + ... in path order (see _group_tables)."""
+def _group_matrices(S, gsum, ng, n):
+    """M[g] = S[p_g0] + S[p_g1] + ... in path order (see _group_tables); groups g >= gsum.ng
+    (padding slots) are zero.  On the device one itr_group_sum launch."""
     import torch
+    if S.is_cuda:
+        from ..dense import group_sum
+        M = (torch.zeros if ng > gsum.ng else torch.empty)((ng, n, n), dtype=S.dtype,
+                                                           device=S.device)
+        group_sum(S, gsum.off, gsum.paths, gsum.ng, out=M[:gsum.ng])
+        return M
     M = torch.zeros((ng, n, n), dtype=S.dtype, device=S.device)
-    for gs, ps in steps:
+    for gs, ps in gsum.steps:
         M[gs] += S[ps]
     return M
 

@@ -154,8 +154,13 @@ def double_table(t: float, mu: float) -> np.ndarray:
                                   t * t / 2))
     w = np.where(flag, emt, 1.0) * inner
     den = 1 + 0.5 / np.exp(3 * t) - 1.5 / np.exp(t)
-    val = 3 * (w @ C) / den
-    return val.reshape(4, 4, 4, 4, 16).sum(axis=4)
+    val = (3 * (w @ C) / den).reshape(4, 4, 4, 4, 16)
+    # the 16 (e, f) terms summed one after another, e outer, like the reference's cumsum
+    # (get_emission_prob_mat.py:417-423); NumPy's sum over 16 would pair them
+    out = val[..., 0].copy()
+    for i in range(1, 16):
+        out = out + val[..., i]
+    return out
 
 
 def jc69_rate(mu: float) -> np.ndarray:

@@ -31,8 +31,12 @@ Fixtures are DATA only (inputs + expected outputs), written as .npz:
                         for every time-parameter case (captured like derive_times.json)
   int_statespace.json   the CTMC state spaces and rate-symbol matrices load_trans_mat(1..3)
                         returns (int_load_trans_mat.py:6-41), as sets of transitions
+  coal_tables.npz       the reference's one- and two-coalescence tables
+                        p_b_c_given_a_JC69_analytical / p_b_c_d_given_a_JC69_analytical
+                        (get_emission_prob_mat.py:95-118, 400-424: closed forms summed in
+                        the reference's order) at a few (t, mu, k)
 
-Usage:  python tests/golden/make_golden.py alphabet|sweeps|expm|model|intmodel <tag> ...|intspace
+Usage:  python tests/golden/make_golden.py alphabet|sweeps|expm|model|intmodel <tag> ...|intspace|coal
 """
 import os
 import sys
@@ -459,6 +463,29 @@ def cmd_intderive():
     print(f"int_derive_times.json written ({len(out)} cases)")
 
 
+COAL_CASES = [(0.8, 0.3, 1.3), (0.4054651081081643, 4 / 3000, 1.0), (14.90138771, 4 / 3000, 1.0), (0.20279819382384456, 4 / 3000, 1.0)]
+
+
+def cmd_coal():
+    _import_reference()
+    from itrails.get_emission_prob_mat import (p_b_c_d_given_a_JC69_analytical,
+                                               p_b_c_given_a_JC69_analytical)
+    nt = "AGCT"
+    singles, doubles = [], []
+    for t, mu, k in COAL_CASES:
+        S = np.zeros((4, 4, 4))
+        for a, b, c, v in p_b_c_given_a_JC69_analytical(t, mu, k):
+            S[nt.index(a), nt.index(b), nt.index(c)] = v
+        D = np.zeros((4, 4, 4, 4))
+        for a, b, c, d, v in p_b_c_d_given_a_JC69_analytical(t, mu):
+            D[nt.index(a), nt.index(b), nt.index(c), nt.index(d)] = v
+        singles.append(S)
+        doubles.append(D)
+    np.savez(os.path.join(HERE, "coal_tables.npz"), cases=np.array(COAL_CASES),
+             single=np.array(singles), double=np.array(doubles))
+    print("coal_tables.npz written")
+
+
 if __name__ == "__main__":
     cmd = sys.argv[1]
     if cmd == "alphabet":
@@ -479,5 +506,7 @@ if __name__ == "__main__":
         cmd_intspace()
     elif cmd == "intderive":
         cmd_intderive()
+    elif cmd == "coal":
+        cmd_coal()
     else:
         raise SystemExit(__doc__)

@@ -147,3 +147,27 @@ def test_split_model_build_ranks_match_single_rank(gpu, world):
         assert np.array_equal(a, a1) and np.array_equal(pi, pi1)
         assert np.allclose(a, g["a"], rtol=1e-10, atol=1e-15)
     assert sum(v for _, _, _, v in res) == la.stats["vanloan"]
+
+
+def test_rccl_world1_beside_partition_streams(gpu):
+    """RCCL (the `nccl` backend) executing on this one GPU beside itr_forward_viterbi's three
+    CU-masked streams, with the queue setting bench.py uses for N > 1
+    (GPU_MAX_HW_QUEUES = 8): bench.py --dist 1 initialises a world-size-1 nccl group, so
+    every timed step's log-likelihood exchange is a real all-reduce of the per-block vector
+    after the partitioned sweep; the line must report the nccl backend, the exchange time,
+    Viterbi paths equal to the CPU restatement and log-likelihoods within 1e-8."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dist", "1",
+           "--backend", "nccl", "--mbp", "2", "--steps", "3", "--warmup", "2",
+           "--host-path", "0", "--cpu-1core-cols", "0"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["config"]["backend"] == "nccl" and r["config"]["world_size_seen"] == 1
+    assert r["allreduce_ms"] is not None and r["allreduce_ms"] > 0
+    assert r["viterbi_equal"] is True and r["columns_checked"] == 2_000_000
+    assert r["loglik_max_rel_err"] < 1e-8

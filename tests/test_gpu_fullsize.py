@@ -14,7 +14,10 @@ do not need the CPU oracle to run over all of it:
   * the device-built (5,5) model against the reference-built one on the whole workload;
   * every block's log-likelihood finite and negative, the total equal to the block-order
     sum of the per-block values (loglik_wrapper semantics);
-  * every posterior row sums to 1 (1e-12) and matches the oracle on the sampled blocks.
+  * every posterior row sums to 1 (1e-12) and matches the oracle (1e-8), every block;
+  * BASELINE config 3 (the reference's (7,7) model, N = 133) and the introgression (5,5)
+    model (N = 95) against the oracle on every block: posterior rows 1e-8, Viterbi paths
+    identical, log-likelihoods 1e-8.
 """
 import os
 
@@ -183,11 +186,7 @@ def test_full_size_posterior_rows(full):
     post = hmm.posterior_device(full["model"], plan, full["d_obs"])
     sums = post.sum(dim=1)
     assert float((sums - 1.0).abs().max()) < 1e-12
-    obs, off, sample = full["obs"], full["off"], full["sample"][:20]
-    so, soff = _sub(obs, off, sample)
-    ref = O.posterior(full["t"], so, soff)
-    rows = torch.cat([post[off[k]:off[k + 1]] for k in sample]).cpu().numpy()
-    np.testing.assert_allclose(rows, ref, rtol=1e-8, atol=1e-300)
+    assert _posterior_every_block(full["t"], full["obs"], full["off"], post) == 10_000_000
     del post
     torch.cuda.empty_cache()
 
@@ -256,30 +255,79 @@ def full77(gpu):
                 sample=sample, t=build_tables(a, b, pi))
 
 
+def _posterior_every_block(t, obs, off, post, chunk_cols=1_000_000):
+    """Every posterior row of a device posterior `post` (total x N, on the device) against
+    the CPU restatement, in runs of whole blocks of about chunk_cols columns so host memory
+    stays bounded (10 Mbp x 133 states is 10.6 GB of rows): rows to 1e-8 relative."""
+    nb = len(off) - 1
+    k0, checked = 0, 0
+    while k0 < nb:
+        k1 = int(np.searchsorted(off, off[k0] + chunk_cols, side="right")) - 1
+        k1 = min(nb, max(k0 + 1, k1))
+        o = off[k0:k1 + 1] - off[k0]
+        ref = O.posterior(t, obs[off[k0]:off[k1]], o)
+        rows = post[off[k0]:off[k1]].cpu().numpy()
+        np.testing.assert_allclose(rows, ref, rtol=1e-8, atol=1e-300,
+                                   err_msg=f"blocks {k0}..{k1 - 1}")
+        checked += rows.shape[0]
+        k0 = k1
+    return checked
+
+
 def test_full_size_77_posterior(full77):
-    """Every posterior row of the 10 Mbp alignment sums to 1 (1e-12); the longest blocks and
-    a seeded sample match the CPU restatement to 1e-8."""
+    """BASELINE config 3 in full: every posterior row of the 10 Mbp alignment (all 5,036
+    blocks) against the CPU restatement to 1e-8 relative, and every row sums to 1 (1e-12)."""
     import torch
     f = full77
     f["plan"].reserve(133, posterior=True)
     post = hmm.posterior_device(f["model"], f["plan"], f["d_obs"])
     assert float((post.sum(dim=1) - 1.0).abs().max()) < 1e-12
-    so, soff = _sub(f["obs"], f["off"], f["sample"])
-    ref = O.posterior(f["t"], so, soff)
-    off = f["off"]
-    rows = torch.cat([post[off[k]:off[k + 1]] for k in f["sample"]]).cpu().numpy()
-    np.testing.assert_allclose(rows, ref, rtol=1e-8, atol=1e-300)
+    assert _posterior_every_block(f["t"], f["obs"], f["off"], post) == 10_000_000
     del post
     torch.cuda.empty_cache()
 
 
 def test_full_size_77_forward_viterbi(full77):
+    """Config 3's model through both decoding calls, every block against the CPU
+    restatement: the separate forward / Viterbi calls and the combined itr_forward_viterbi
+    (paths identical on all 10 M columns, log-likelihoods 1e-8)."""
     f = full77
     ll = hmm.forward_loglik_device(f["model"], f["plan"], f["d_obs"]).cpu().numpy()
     path = hmm.viterbi_device(f["model"], f["plan"], f["d_obs"]).cpu().numpy()
     assert np.isfinite(ll).all() and (ll < 0).all()
-    so, soff = _sub(f["obs"], f["off"], f["sample"])
-    np.testing.assert_allclose(ll[f["sample"]], O.forward_loglik(f["t"], so, soff), rtol=1e-8,
-                               atol=0)
-    got = np.concatenate([path[f["off"][k]:f["off"][k + 1]] for k in f["sample"]])
-    np.testing.assert_array_equal(got, O.viterbi(f["t"], so, soff))
+    _check_all_blocks(f["t"], f["obs"], f["off"], ll, path)
+    ll2, path2 = hmm.forward_viterbi_device(f["model"], f["plan"], f["d_obs"])
+    assert np.array_equal(path2.cpu().numpy(), path)
+    np.testing.assert_allclose(ll2.cpu().numpy(), ll, rtol=1e-12, atol=0)
+
+
+# ---------------------------------------------------------------------------------------
+# the introgression (5,5) model (SURVEY 8(f) row 4; N = 95, the reference's own build,
+# tests/golden/model_int_ikat_5_5.npz) over the full 10 Mbp layout
+# ---------------------------------------------------------------------------------------
+def test_full_size_intro95_every_block(gpu):
+    """itrails-int-viterbi's hot path at N = 95 over 10 Mbp (5,036 blocks): forward
+    log-likelihoods (1e-8) and Viterbi paths (identical) of every block against the CPU
+    restatement, through the combined call and the Viterbi-only call; the posterior rows
+    of the first ~1 Mbp against the restatement (1e-8) and every row summing to 1."""
+    import torch
+    g = golden("model_int_ikat_5_5.npz")
+    a, b, pi = g["a"], g["b"], g["pi"]
+    assert a.shape[0] == 95
+    lengths = block_lengths(np.random.default_rng(12345), 10_000_000, 2000.0)
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=777)
+    t = build_tables(a, b, pi)
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).cuda()
+    ll, path = hmm.forward_viterbi_device(model, plan, d_obs)
+    ll, path = ll.cpu().numpy(), path.cpu().numpy()
+    _check_all_blocks(t, obs, off, ll, path)
+    assert np.array_equal(hmm.viterbi_device(model, plan, d_obs).cpu().numpy(), path)
+    nb = int(np.searchsorted(off, 1_000_000))
+    sub = hmm.Plan(off[:nb + 1])
+    sub.reserve(95, posterior=True)
+    post = hmm.posterior_device(model, sub, d_obs[:off[nb]])
+    assert float((post.sum(dim=1) - 1.0).abs().max()) < 1e-12
+    assert _posterior_every_block(t, obs[:off[nb]], off[:nb + 1], post) == off[nb]
+    del post, d_obs
+    torch.cuda.empty_cache()

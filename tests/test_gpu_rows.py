@@ -75,3 +75,22 @@ def test_rows_single_column_and_ties(gpu):
     np.testing.assert_array_equal(prev, prev_ref)
     np.testing.assert_array_equal(hmm.backtrack_viterbi(omega, prev),
                                   R.backtrack_viterbi(om_ref, prev_ref))
+
+
+def test_backtrack_malformed_pointers(gpu):
+    """Back-pointers outside the states: the reference's prev[i, int(s)] raises IndexError
+    (|s| >= n) or fails on NaN; a negative index wraps like NumPy's.  The kernel never reads
+    a row outside prev."""
+    n, T = 5, 6
+    omega = np.zeros((T, n))
+    omega[-1, 2] = 1.0  # last state 2
+    prev = np.zeros((T - 1, n))
+    prev[:, 2] = -1.0  # -> state n - 1 = 4 (wraps)
+    prev[:, 4] = 4.0
+    np.testing.assert_array_equal(hmm.backtrack_viterbi(omega, prev),
+                                  R.backtrack_viterbi(omega, prev))
+    for bad in (5.0, -6.0, np.nan, np.inf, 1e300):
+        p = prev.copy()
+        p[1, 4] = bad
+        with pytest.raises(IndexError):
+            hmm.backtrack_viterbi(omega, p)

@@ -84,3 +84,21 @@ def test_device_chain_routes_like_host_chain(name):
     a_d, _, pi_d, _, _ = trans_emiss_calc(*g["args"], n_ab, n_abc, la=la_d)
     assert la_d.stats["vanloan"] > la_h.stats["vanloan"] > 0  # + the propagator jobs
     assert np.allclose(a_d, a_h, rtol=1e-12, atol=0) and np.allclose(pi_d, pi_h, rtol=1e-12)
+
+
+def test_coalescence_tables_vs_reference_closed_forms():
+    """single_table / double_table against the reference's own closed forms summed in its
+    order (tests/golden/coal_tables.npz: p_b_c_given_a_JC69_analytical and
+    p_b_c_d_given_a_JC69_analytical, get_emission_prob_mat.py:95-118, 400-424) at the KAT
+    model's (t, mu) and one larger mu.  Entries of order (mu t)^3 come out of a cancellation
+    of O(1) terms in both closed forms (at mu = 4/3000 both lose up to ~1e-4 of such an entry
+    against a 30-digit quadrature), so the bar is the table's scale: |x - ref| <= 4e-15 max
+    |ref|, and 1e-12 relative where nothing cancels (mu = 0.3)."""
+    g = golden("coal_tables.npz")
+    for (t, mu, k), S, D in zip(g["cases"], g["single"], g["double"]):
+        s, d = single_table(t, mu, k), double_table(t, mu)
+        assert np.abs(s - S).max() <= 4e-15 * np.abs(S).max()
+        assert np.abs(d - D).max() <= 4e-15 * np.abs(D).max()
+        if mu > 0.1:
+            np.testing.assert_allclose(s, S, rtol=1e-12, atol=0)
+            np.testing.assert_allclose(d, D, rtol=1e-12, atol=0)

@@ -42,12 +42,13 @@ def lib():
 
 def test_chr10(lib):
     """BASELINE config 2 (bench default): 59 long blocks, two at a time per reserved CU on 21
-    CUs (one per CU they would need 35: more than 1/8 of the chip), + 20 CUs for the
-    forward's VALU halves in the forward+Viterbi call, 69 long blocks in the Viterbi-only call
+    CUs (one per CU they would need 35: more than 1/8 of the chip), + 14 CUs for the
+    forward's VALU halves, also two at a time (one per CU: 20 > kFwdPairMin), in the
+    forward+Viterbi call, 69 long blocks in the Viterbi-only call
     (profiles/r4m_vit_long_set.txt: 59..80 long blocks all within 1 % of the best)."""
     d = info(geometric(10_000_000))
     assert d["wave_ok"] == 1
-    assert d["vit_nlong"] == 59 and d["vit_reserve"] == 21 and d["fwd_reserve"] == 20
+    assert d["vit_nlong"] == 59 and d["vit_reserve"] == 21 and d["fwd_reserve"] == 14
     assert d["vit_nlong_v"] == 69
     assert 40 <= d["vit_nlong"] <= 80 and 59 <= d["vit_nlong_v"] <= 80
 
