@@ -152,6 +152,22 @@ ITR_API int itr_forward_viterbi(itr_model_t model, itr_plan_t plan, const uint16
 ITR_API int itr_posterior(itr_model_t model, itr_plan_t plan, const uint16_t* d_obs,
                           double* d_post, void* stream);
 
+/* The drop-in host calls on the reference's own inputs: V_lst as n_blocks host int64 arrays
+ * (blocks[k], lens[k] columns; read_data.py:94-117), which must match the plan's layout.
+ * The blocks are packed and range-checked by host threads into a pinned buffer (ITR_EDATA
+ * for a symbol outside the 625-letter alphabet, like the reference's IndexError), copied to
+ * a device buffer kept by the calling thread (itr_release_staging frees both), swept on the
+ * null stream, and the results returned to host memory:
+ *   itr_forward_loglik_blocks: h_loglik[k] = forward_loglik of block k (optimizer.py:145-162)
+ *   itr_viterbi_blocks:        h_path[c]  = Viterbi state of column c as float64, the dtype
+ *                              backtrack_viterbi returns (optimizer.py:336-377)
+ * Both return when the results are on the host. */
+ITR_API int itr_forward_loglik_blocks(itr_model_t model, itr_plan_t plan,
+                                      const int64_t* const* blocks, const int64_t* lens,
+                                      int64_t n_blocks, double* h_loglik);
+ITR_API int itr_viterbi_blocks(itr_model_t model, itr_plan_t plan, const int64_t* const* blocks,
+                               const int64_t* lens, int64_t n_blocks, double* h_path);
+
 /* The reference's standalone sweep matrices of ONE block of T >= 1 columns, device pointers,
  * float64 row-major, on `stream`:
  *   kind 0  forward:  log alpha [T][N]                            (optimizer.py:165-188)

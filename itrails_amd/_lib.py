@@ -51,6 +51,8 @@ _SIGNATURES = {
     "itr_forward_loglik_host": ([_P, _P, _P, _P], _I),
     "itr_viterbi_host": ([_P, _P, _P, _P], _I),
     "itr_posterior_host": ([_P, _P, _P, _P], _I),
+    "itr_forward_loglik_blocks": ([_P, _P, _P, _P, _I64, _P], _I),
+    "itr_viterbi_blocks": ([_P, _P, _P, _P, _I64, _P], _I),
     "itr_release_staging": ([], _I),
     "itr_release_streams": ([], _I),
     "itr_last_kernel_ms": ([ctypes.c_char_p, ctypes.POINTER(_D)], _I),

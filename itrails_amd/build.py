@@ -8,12 +8,13 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["hmm_sweeps.hip", "mfma_sweeps.hip", "wave_sweeps.hip", "dense.hip", "vanloan.hip", "emission.hip", "rows.hip", "maf.cpp", "writers.cpp", "capi.cpp"]
+SOURCES = ["hmm_sweeps.hip", "mfma_sweeps.hip", "wave_sweeps.hip", "dense.hip", "vanloan.hip", "emission.hip", "rows.hip", "prune_vit.hip", "maf.cpp", "writers.cpp", "capi.cpp"]
 OUT = os.path.join(HERE, "libitrails_hip.so")
 # The sweeps never produce NaN (log 0 = -inf is the only non-finite value, and no
 # inf - inf or 0/0 is formed), so fmax needs no NaN-quieting canonicalize after each DPP
 # move; infinities keep their IEEE semantics (no -ffinite-math-only).
-EXTRA = {"hmm_sweeps.hip": ["-fno-honor-nans"], "mfma_sweeps.hip": ["-fno-honor-nans"], "wave_sweeps.hip": ["-fno-honor-nans"]}
+EXTRA = {"hmm_sweeps.hip": ["-fno-honor-nans"], "mfma_sweeps.hip": ["-fno-honor-nans"], "wave_sweeps.hip": ["-fno-honor-nans"],
+         "prune_vit.hip": ["-fno-honor-nans"]}
 ARCH = os.environ.get("ITR_OFFLOAD_ARCH", "gfx950")
 
 
@@ -61,6 +62,26 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False,
     return out
 
 
+def build_blocks_ext(force: bool = False, verbose: bool = False) -> str:
+    """itrails_amd/_blocks*.so: the CPython extension that scans a V_lst's int64 arrays for
+    the host-block entry points (csrc/blocks_ext.c; gcc against this interpreter's headers)."""
+    import sysconfig
+
+    import numpy as np
+    src = os.path.join(CSRC, "blocks_ext.c")
+    out = os.path.join(HERE, "_blocks" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if not force and os.path.exists(out) and os.path.getmtime(out) > os.path.getmtime(src):
+        return out
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-shared", "-fPIC", "-Wall",
+           "-I" + sysconfig.get_paths()["include"], "-I" + np.get_include(), src,
+           "-o", out + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 if __name__ == "__main__":
     if "--with-exp" in sys.argv:  # product + experiment library (env knobs), in parallel
         import threading
@@ -70,3 +91,5 @@ if __name__ == "__main__":
         t.join()
     else:
         print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))
+        if "--diag" not in sys.argv:
+            print(build_blocks_ext(force="--force" in sys.argv, verbose=True))

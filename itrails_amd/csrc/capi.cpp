@@ -14,6 +14,7 @@
 #include <optional>
 #include <atomic>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -35,6 +36,22 @@ int fail(int code, const char* fmt, ...) {
   va_end(ap);
   g_err = buf;
   return code;
+}
+
+// host threads of this job: OMP_NUM_THREADS when set (the GPU pool sets it to the job's CPU
+// share), else the machine's cores; at most 16
+int host_threads() {
+  const char* e = getenv("OMP_NUM_THREADS");
+  int n = e ? atoi(e) : 0;
+  if (n <= 0) n = (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(16, n));
+}
+template <class F>
+void parallel_for(int nt, F&& f) {
+  std::vector<std::thread> th;
+  for (int w = 1; w < nt; ++w) th.emplace_back(f, w);
+  f(0);
+  for (auto& t : th) t.join();
 }
 
 #define HIP_TRY(expr)                                                                      \
@@ -267,6 +284,7 @@ struct itr_model {
   double* LEWP = nullptr;
   int32_t* VSLOT = nullptr;
   double* VMB = nullptr;
+  double* MJ = nullptr;  // [n] max_{i != j} log a_ij (the bound-pruned Viterbi, prune_vit.hip)
   int xrw = 0;
   std::vector<double> h_a, h_la, h_LE, h_E, h_PIE;  // (E, PIE: the 256 N-free symbols)
   std::mutex vit_mu;  // (the first Viterbi calls of several threads)
@@ -296,6 +314,7 @@ struct itr_plan {
   double* d_sink = nullptr;  // write target of padded states (64 doubles)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
   std::vector<int64_t> sorted_len;  // block lengths, longest first (processing order)
+  std::vector<int64_t> h_off;       // block offsets (host copy: the host-block entry points)
   // forward log-likelihood tasks {block, split, slot} (split blocks: two halves) and the
   // split blocks' scratch
   int64_t ntasks = 0, nsplit = 0;
@@ -745,6 +764,19 @@ int itr_model_create(int n, const double* a, const double* la, const double* E,
     itr_model_destroy(m);
     return e;
   }
+  if (itr::prune_vit_geometry(n).waves > 0) {  // the bound of the pruned Viterbi step
+    std::vector<double> mj(n, -INFINITY);
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j)
+        if (i != j) mj[j] = std::max(mj[j], la[(size_t)i * n + j]);
+    e = dev_alloc(&m->MJ, (size_t)n);
+    if (!e && hipMemcpy(m->MJ, mj.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+      e = fail(ITR_EHIP, "table upload failed");
+    if (e) {
+      itr_model_destroy(m);
+      return e;
+    }
+  }
   const itr::WaveVitGeometry wv = itr::wave_vit_geometry(n);
   if (wv.iq > 0) {  // (the per-wave Viterbi's tables: on the first Viterbi call)
     m->xrw = wv.xr;
@@ -793,6 +825,7 @@ int itr_model_destroy(itr_model_t m) {
   dev_free(m->LEWP);
   dev_free(m->VSLOT);
   dev_free(m->VMB);
+  dev_free(m->MJ);
   dev_free(m->EF);
   delete m;
   return 0;
@@ -828,6 +861,7 @@ int plan_create_impl(const int64_t* off, int64_t nblocks, double split_frac,
   (void)hipGetDevice(&p->device);
   p->nblocks = nblocks;
   p->total = h_off[nblocks];
+  p->h_off = h_off;
   std::vector<int64_t> tile_off(nblocks + 1, 0);
   for (int64_t k = 0; k < nblocks; ++k)
     tile_off[k + 1] = tile_off[k] + itr::vit_tiles(h_off[k + 1] - h_off[k]);
@@ -1272,27 +1306,34 @@ int vit_slot_tables(itr_model_t m) {
       if (i != j) mj[j] = std::max(mj[j], la[(size_t)i * n + j]);
   std::vector<int> rank(n);
   std::iota(rank.begin(), rank.end(), 0);
-  std::vector<int64_t> fails(n, 0);
-  uint64_t rs = 0x2545F4914F6CDD1Dull;
-  auto rnd = [&]() {  // splitmix64 -> [0, 1)
-    uint64_t z = (rs += 0x9E3779B97F4A7C15ull);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return (double)((z ^ (z >> 31)) >> 11) * 0x1.0p-53;
-  };
-  auto draw = [&](auto&& prob, int cnt) {  // index by cumulative weight
-    double tot = 0.0;
-    for (int k = 0; k < cnt; ++k) tot += prob(k);
-    double u = rnd() * tot;
-    for (int k = 0; k < cnt; ++k) {
-      u -= prob(k);
-      if (u < 0.0) return k;
-    }
-    return cnt - 1;
-  };
-  std::vector<double> om(n), nx(n);
-  for (int b = 0; b < 8; ++b) {
-    int s = draw([&](int j) { double v = 0.0; for (int o = 0; o < 256; ++o) v += m->h_PIE[(size_t)o * n + j]; return v; }, n);
+  // how often each state fails the pruned step's bound on 8 sequences of 256 columns
+  // sampled from the model (one host thread per sequence, each with its own generator)
+  constexpr int kSeq = 8;
+  std::vector<std::vector<int64_t>> fails_b(kSeq, std::vector<int64_t>(n, 0));
+  std::vector<double> pi_w(n, 0.0);
+  for (int j = 0; j < n; ++j)
+    for (int o = 0; o < 256; ++o) pi_w[j] += m->h_PIE[(size_t)o * n + j];
+  auto sequence = [&](int b) {
+    uint64_t rs = 0x2545F4914F6CDD1Dull + 0x632BE59BD9B4E019ull * (uint64_t)b;
+    auto rnd = [&]() {  // splitmix64 -> [0, 1)
+      uint64_t z = (rs += 0x9E3779B97F4A7C15ull);
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      return (double)((z ^ (z >> 31)) >> 11) * 0x1.0p-53;
+    };
+    auto draw = [&](auto&& prob, int cnt) {  // index by cumulative weight
+      double tot = 0.0;
+      for (int k = 0; k < cnt; ++k) tot += prob(k);
+      double u = rnd() * tot;
+      for (int k = 0; k < cnt; ++k) {
+        u -= prob(k);
+        if (u < 0.0) return k;
+      }
+      return cnt - 1;
+    };
+    std::vector<int64_t>& fails = fails_b[b];
+    std::vector<double> om(n), nx(n);
+    int s = draw([&](int j) { return pi_w[j]; }, n);
     int o = draw([&](int k) { return m->h_E[(size_t)k * n + s]; }, 256);
     for (int j = 0; j < n; ++j) om[j] = std::log(m->h_PIE[(size_t)o * n + j]);
     for (int t = 1; t < 256; ++t) {
@@ -1310,7 +1351,17 @@ int vit_slot_tables(itr_model_t m) {
       }
       om.swap(nx);
     }
-  }
+  };
+  parallel_for(std::min(kSeq, host_threads()) == kSeq ? kSeq : 1, [&](int w) {
+    if (std::min(kSeq, host_threads()) == kSeq) {
+      sequence(w);
+    } else {
+      for (int b = 0; b < kSeq; ++b) sequence(b);
+    }
+  });
+  std::vector<int64_t> fails(n, 0);
+  for (int b = 0; b < kSeq; ++b)
+    for (int j = 0; j < n; ++j) fails[j] += fails_b[b][j];
   std::stable_sort(rank.begin(), rank.end(), [&](int x, int y) { return fails[x] > fails[y]; });
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_VSLOT_NATURAL")) std::iota(rank.begin(), rank.end(), 0);
@@ -1631,7 +1682,41 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       HIP_TRY(itr::launch_fwd_split_combine(m->n, gf.xr, (int)p->nhsplit, p->d_hsplit_blk,
                                             p->d_svec, p->d_sK, fwd_loglik, st));
   } else if (!few) {
-    if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
+    const itr::PruneVitGeometry pg = itr::prune_vit_geometry(m->n);
+    // (few blocks: their lone step latency bounds the call — the 9-wave layout's is lower)
+    bool prune = pg.waves > 0 && m->MJ && p->nblocks > 2 * cus;
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_NO_PRUNE_VIT")) prune = false;
+#endif
+    if (prune) {
+      // one block per wavefront, log a in LDS, the bound-pruned step (prune_vit.hip)
+      itr::PruneVitArgs v{};
+      v.n = m->n;
+      v.xr = vit_stride(m->n);
+      v.nblocks = p->nblocks;
+      v.order = p->d_order;
+      v.queue = p->d_queue + 2;
+      v.off = p->d_off;
+      v.tile_off = p->d_tile_off;
+      v.obs = obs;
+      v.la = m->la;
+      v.mj = m->MJ;
+      v.log_e = m->LE;
+      v.lpie = m->LPIE;
+      v.ckpt = p->d_alpha;
+      v.stay = p->d_stay;
+      v.last_state = p->d_last;
+      // the blocks long enough to be the makespan (about one per SIMD) at raised priority
+      v.prio_len = (int)std::max<int64_t>(
+          1, p->sorted_len[std::min<int64_t>(p->nblocks - 1, (int64_t)cus * 4)]);
+      HIP_TRY(hipMemsetAsync(v.queue, 0, sizeof(int), st));
+      const int64_t grid = std::min<int64_t>(cus, (p->nblocks + pg.waves - 1) / pg.waves);
+      std::optional<Scope> sc;
+      if (!fwd_loglik) sc.emplace("viterbi", st);
+      HIP_TRY(itr::launch_prune_vit(pg, (int)grid, v, st));
+    } else {
+      if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
+    }
   }
   both.reset();
   itr::TraceArgs ta = trace_args();
@@ -1797,6 +1882,47 @@ struct Staging {
 };
 thread_local Staging g_stage;
 
+// The calling thread's pinned host buffer and device buffer of the host-block entry points
+// (grow-only, per device): no allocation, no pageable copy per call.
+struct HostIO {
+  int device = -1;
+  void* pin = nullptr;
+  size_t pin_cap = 0;
+  void* dbuf = nullptr;
+  size_t dcap = 0;
+  void release() {
+    if (pin) (void)hipHostFree(pin);
+    if (dbuf) (void)hipFree(dbuf);
+    pin = dbuf = nullptr;
+    pin_cap = dcap = 0;
+    device = -1;
+  }
+  int reserve(size_t pin_bytes, size_t dev_bytes) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev != device) {
+      release();
+      device = dev;
+    }
+    if (pin_bytes > pin_cap) {
+      if (pin) (void)hipHostFree(pin);
+      pin = nullptr;
+      pin_cap = 0;
+      HIP_TRY(hipHostMalloc(&pin, pin_bytes, hipHostMallocDefault));
+      pin_cap = pin_bytes;
+    }
+    if (dev_bytes > dcap) {
+      if (dbuf) (void)hipFree(dbuf);
+      dbuf = nullptr;
+      dcap = 0;
+      HIP_TRY(hipMalloc(&dbuf, dev_bytes));
+      dcap = dev_bytes;
+    }
+    return 0;
+  }
+};
+thread_local HostIO g_hio;
+
 int copy_out_large(void* dst, const void* src, size_t bytes) {
   if (bytes < 2 * kStageBytes) {
     HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
@@ -1895,6 +2021,7 @@ int itr_release_streams(void) {
 
 int itr_release_staging(void) {
   g_stage.release();
+  g_hio.release();
   itr::release_vanloan_workspace();
   return 0;
 }
@@ -2158,22 +2285,17 @@ int itr_maf_close(itr_maf_t h) {
 // V_lst -> (uint16 columns, int64 offsets): the blocks are split into contiguous ranges of
 // about equal column count, one per thread; each thread converts and range-checks its own
 // blocks, and the first bad symbol (lowest block) is reported.
-int itr_pack_symbols(const int64_t* const* blocks, const int64_t* lens, int64_t n_blocks,
-                     uint16_t* obs, int64_t* block_off) {
-  if (n_blocks < 0 || !block_off || (n_blocks > 0 && !lens))
-    return fail(ITR_EINVAL, "bad pack arguments");
-  block_off[0] = 0;
-  for (int64_t k = 0; k < n_blocks; ++k) {
-    if (lens[k] < 0) return fail(ITR_EINVAL, "block %lld has negative length", (long long)k);
-    if (lens[k] > 0 && !blocks[k]) return fail(ITR_EINVAL, "block %lld is null", (long long)k);
-    block_off[k + 1] = block_off[k] + lens[k];
-  }
+namespace {
+// V_lst -> uint16 columns at the given offsets: the blocks are split into contiguous ranges
+// of about equal column count, one per thread; each thread converts and range-checks its
+// own blocks, and the first bad symbol (lowest block) is reported.
+int pack_blocks(const int64_t* const* blocks, const int64_t* lens, const int64_t* block_off,
+                int64_t n_blocks, uint16_t* obs) {
   const int64_t total = block_off[n_blocks];
   if (total == 0) return 0;
-  if (!obs) return fail(ITR_EINVAL, "null output");
-  const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, total >> 20));
+  const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, total >> 18));
   std::vector<int64_t> bad(nt, -1), bad_col(nt, -1);
-  auto work = [&](int w) {
+  parallel_for(nt, [&](int w) {
     const int64_t lo_col = total * w / nt, hi_col = total * (w + 1) / nt;
     // blocks whose first column falls in [lo_col, hi_col)
     int64_t k = std::lower_bound(block_off, block_off + n_blocks, lo_col) - block_off;
@@ -2195,16 +2317,128 @@ int itr_pack_symbols(const int64_t* const* blocks, const int64_t* lens, int64_t 
         return;
       }
     }
-  };
-  std::vector<std::thread> th;
-  for (int w = 1; w < nt; ++w) th.emplace_back(work, w);
-  work(0);
-  for (auto& t : th) t.join();
+  });
   for (int w = 0; w < nt; ++w)
     if (bad[w] >= 0)
       return fail(ITR_EDATA, "observed symbol %lld (block %lld, column %lld) outside the "
                   "625-letter alphabet", (long long)blocks[bad[w]][bad_col[w]],
                   (long long)bad[w], (long long)bad_col[w]);
+  return 0;
+}
+
+
+// the blocks of a host-block call against the plan's layout; packed into pinned memory and
+// copied to the device buffer (stream order on the null stream, like the sweeps after it)
+int upload_blocks(itr_plan_t p, const int64_t* const* blocks, const int64_t* lens,
+                  int64_t n_blocks, size_t extra_dev, uint16_t** d_obs) {
+  if (n_blocks != p->nblocks)
+    return fail(ITR_EINVAL, "%lld blocks for a plan of %lld", (long long)n_blocks,
+                (long long)p->nblocks);
+  if (n_blocks > 0 && !lens) return fail(ITR_EINVAL, "null lengths");
+  for (int64_t k = 0; k < n_blocks; ++k) {
+    if (lens[k] != p->h_off[k + 1] - p->h_off[k])
+      return fail(ITR_EINVAL, "block %lld has %lld columns, the plan %lld", (long long)k,
+                  (long long)lens[k], (long long)(p->h_off[k + 1] - p->h_off[k]));
+    if (lens[k] > 0 && !blocks[k]) return fail(ITR_EINVAL, "block %lld is null", (long long)k);
+  }
+  const size_t ob = (size_t)std::max<int64_t>(p->total, 1) * sizeof(uint16_t);
+  const size_t ob16 = (ob + 255) & ~(size_t)255;
+  if (int e = g_hio.reserve(std::max(ob, (size_t)p->total), ob16 + extra_dev)) return e;
+  uint16_t* h = (uint16_t*)g_hio.pin;
+  if (int e = pack_blocks(blocks, lens, p->h_off.data(), n_blocks, h)) return e;
+  *d_obs = (uint16_t*)g_hio.dbuf;
+  if (p->total)
+    HIP_TRY(hipMemcpyAsync(*d_obs, h, p->total * sizeof(uint16_t), hipMemcpyHostToDevice,
+                           nullptr));
+  return 0;
+}
+size_t dev_tail(itr_plan_t p) {  // first byte after the observations in g_hio.dbuf
+  const size_t ob = (size_t)std::max<int64_t>(p->total, 1) * sizeof(uint16_t);
+  return (ob + 255) & ~(size_t)255;
+}
+}  // namespace
+
+int itr_pack_symbols(const int64_t* const* blocks, const int64_t* lens, int64_t n_blocks,
+                     uint16_t* obs, int64_t* block_off) {
+  if (n_blocks < 0 || !block_off || (n_blocks > 0 && !lens))
+    return fail(ITR_EINVAL, "bad pack arguments");
+  block_off[0] = 0;
+  for (int64_t k = 0; k < n_blocks; ++k) {
+    if (lens[k] < 0) return fail(ITR_EINVAL, "block %lld has negative length", (long long)k);
+    if (lens[k] > 0 && !blocks[k]) return fail(ITR_EINVAL, "block %lld is null", (long long)k);
+    block_off[k + 1] = block_off[k] + lens[k];
+  }
+  if (block_off[n_blocks] == 0) return 0;
+  if (!obs) return fail(ITR_EINVAL, "null output");
+  return pack_blocks(blocks, lens, block_off, n_blocks, obs);
+}
+
+namespace {
+// ITR_HOST_TIMING=1: stage times of the host-block entry points on stderr (diagnostics)
+struct HostClock {
+  bool on = getenv("ITR_HOST_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(const char* what) {
+    if (!on) return;
+    (void)hipDeviceSynchronize();
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "%s %.3f ms  ", what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+  void end() {
+    if (on) fprintf(stderr, "\n");
+  }
+};
+}  // namespace
+
+int itr_forward_loglik_blocks(itr_model_t m, itr_plan_t p, const int64_t* const* blocks,
+                              const int64_t* lens, int64_t n_blocks, double* h_ll) {
+  if (int e = check_model(m)) return e;
+  if (int e = check_plan(p)) return e;
+  if (p->nblocks > 0 && !h_ll) return fail(ITR_EINVAL, "null output");
+  uint16_t* d_obs = nullptr;
+  const size_t tail = dev_tail(p);
+  HostClock clk;
+  if (int e = upload_blocks(p, blocks, lens, n_blocks, (size_t)p->nblocks * 8 + 8, &d_obs))
+    return e;
+  clk.lap("loglik: pack+h2d");
+  if (p->nblocks == 0) return 0;
+  double* d_ll = (double*)((char*)g_hio.dbuf + tail);
+  if (int e = itr_forward_loglik(m, p, d_obs, d_ll, nullptr)) return e;
+  clk.lap("sweep");
+  HIP_TRY(hipMemcpy(h_ll, d_ll, p->nblocks * sizeof(double), hipMemcpyDeviceToHost));
+  clk.lap("d2h");
+  clk.end();
+  return 0;
+}
+
+int itr_viterbi_blocks(itr_model_t m, itr_plan_t p, const int64_t* const* blocks,
+                       const int64_t* lens, int64_t n_blocks, double* h_path) {
+  if (int e = check_model(m)) return e;
+  if (int e = check_plan(p)) return e;
+  if (p->total > 0 && !h_path) return fail(ITR_EINVAL, "null output");
+  uint16_t* d_obs = nullptr;
+  const size_t tail = dev_tail(p);
+  HostClock clk;
+  if (int e = upload_blocks(p, blocks, lens, n_blocks, (size_t)p->total + 8, &d_obs)) return e;
+  clk.lap("viterbi: pack+h2d");
+  if (p->total == 0) return 0;
+  uint8_t* d_path = (uint8_t*)g_hio.dbuf + tail;
+  if (int e = itr_viterbi(m, p, d_obs, d_path, nullptr)) return e;
+  clk.lap("sweep");
+  // the states back through the pinned buffer (the observations' upload finished before the
+  // sweep on this stream), widened to float64 (the reference's path dtype) by host threads
+  uint8_t* h = (uint8_t*)g_hio.pin;
+  HIP_TRY(hipMemcpy(h, d_path, p->total, hipMemcpyDeviceToHost));
+  clk.lap("d2h");
+  const int64_t total = p->total;
+  const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, total >> 18));
+  parallel_for(nt, [&](int w) {
+    const int64_t lo = total * w / nt, hi = total * (w + 1) / nt;
+    for (int64_t c = lo; c < hi; ++c) h_path[c] = (double)h[c];
+  });
+  clk.lap("to_f64");
+  clk.end();
   return 0;
 }
 

@@ -500,6 +500,93 @@ __global__ void __launch_bounds__(256) panel_lds_kernel(int n, double* Mb, int* 
   }
 }
 
+// panel_kernel with each panel row in the registers of one thread (panel-local row t in
+// thread t; at most 256 rows): per column one wave-level pivot reduction (shuffles, lowest
+// index among equal maxima), one barrier to combine the four waves and hand over the pivot
+// row, and the rank-1 update of the thread's own row in registers — instead of an LDS tree
+// reduction with a barrier per level.  Same pivots, multipliers and update expressions in the
+// same order as panel_kernel: bit-identical factors.
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
+                          __builtin_amdgcn_readlane(__double2loint(v), lane));
+}
+template <int KB>
+__global__ void __launch_bounds__(256) panel_reg_kernel(int n, double* Mb, int* pivb, int k0,
+                                                        int kb) {
+  __shared__ double prow[KB], xrow[KB];
+  __shared__ double wv[4];
+  __shared__ int wi[4];
+  double* M = Mb + (int64_t)blockIdx.x * n * n;
+  int* piv = pivb + (int64_t)blockIdx.x * n;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int rows = n - k0;
+  const bool own = t < rows;
+  double x[KB];
+#pragma unroll
+  for (int c = 0; c < KB; ++c) x[c] = (own && c < kb) ? M[(int64_t)(k0 + t) * n + k0 + c] : 0.0;
+#pragma clang loop unroll(full)
+  for (int jj = 0; jj < KB; ++jj) {
+    if (jj >= kb) continue;  // (uniform; keeps the loop unrolled and x in registers)
+    const double v = (own && t >= jj) ? fabs(x[jj]) : -1.0;
+    // the wave's maximum by DPP moves within 16-lane rows and lane reads across them, then
+    // its lowest lane holding it (ballot): the first maximum, as the sequential scan finds
+    double mv = fmax(v, dpp_mov_f64<0xB1>(v));  // quad_perm [1,0,3,2]
+    mv = fmax(mv, dpp_mov_f64<0x4E>(mv));       // quad_perm [2,3,0,1]
+    mv = fmax(mv, dpp_mov_f64<0x141>(mv));      // row_half_mirror
+    mv = fmax(mv, dpp_mov_f64<0x128>(mv));      // row_ror:8
+    mv = fmax(fmax(readlane_f64(mv, 0), readlane_f64(mv, 16)),
+              fmax(readlane_f64(mv, 32), readlane_f64(mv, 48)));
+    const uint64_t hit = __ballot(v == mv);
+    if (lane == 0) {
+      wv[w] = mv;
+      wi[w] = w * 64 + __ffsll((unsigned long long)hit) - 1;
+    }
+    __syncthreads();
+    double bv = wv[0];
+    int p = wi[0];
+#pragma unroll
+    for (int u = 1; u < 4; ++u)
+      if (wv[u] > bv || (wv[u] == bv && wi[u] < p)) {
+        bv = wv[u];
+        p = wi[u];
+      }
+    if (t == 0) piv[k0 + jj] = k0 + p;
+    if (t == p) {
+#pragma unroll
+      for (int c = 0; c < KB; ++c) prow[c] = x[c];
+    }
+    if (t == jj && p != jj) {
+#pragma unroll
+      for (int c = 0; c < KB; ++c) xrow[c] = x[c];
+    }
+    __syncthreads();
+    if (p != jj && (t == jj || t == p)) {
+#pragma unroll
+      for (int c = 0; c < KB; ++c) x[c] = t == jj ? prow[c] : xrow[c];
+    }
+    const double rd = 1.0 / prow[jj];
+    if (own && t > jj) {
+      const double lij = x[jj] * rd;
+      x[jj] = lij;
+#pragma unroll
+      for (int c = jj + 1; c < KB; ++c)
+        if (c < kb) x[c] -= lij * prow[c];
+    }
+    __syncthreads();  // (prow / xrow / wv are rewritten for the next column)
+  }
+  if (own) {
+#pragma unroll
+    for (int c = 0; c < KB; ++c)
+      if (c < kb) M[(int64_t)(k0 + t) * n + k0 + c] = x[c];
+  }
+}
+
 // Apply the panel's row interchanges to every column outside the panel (and to R).
 __global__ void __launch_bounds__(256) swap_kernel(int n, int nrhs, double* Mb, double* Rb,
                                                    const int* pivb, int k0, int kb) {
@@ -608,7 +695,9 @@ hipError_t solve_batched(int n, int nrhs, int64_t batch, double* M, double* R, i
     for (int k0 = 0; k0 < n; k0 += NB) {
       const int kb = std::min(NB, n - k0), k1 = k0 + kb;
       const size_t pbytes = (size_t)(n - k0) * kb * sizeof(double);
-      if (pbytes <= (size_t)kPanelLdsBytes)
+      if (n - k0 <= 256)
+        hipLaunchKernelGGL(panel_reg_kernel<NB>, dim3(nb), dim3(256), 0, st, n, Mc, pc, k0, kb);
+      else if (pbytes <= (size_t)kPanelLdsBytes)
         hipLaunchKernelGGL(panel_lds_kernel, dim3(nb), dim3(256), pbytes, st, n, Mc, pc, k0, kb);
       else
         hipLaunchKernelGGL(panel_kernel, dim3(nb), dim3(256), 0, st, n, Mc, pc, k0, kb);
@@ -827,7 +916,175 @@ static void branch_of(double norm, int* m, int* s) {
   }
 }
 
+// ---- small matrices (n <= 16): the whole expm of one matrix inside one workgroup ---------
+// The model build's small exponentials — the emission branch propagators (4 x 4, hundreds
+// per build), the two-sequence chain (15 x 15) and the one-sequence chain (2 x 2) — are
+// launch- and sync-bound on the batched path (a norm pass read back by the host, then ~20
+// GEMM / LU / combination launches per branch).  Here one 256-thread workgroup per matrix
+// holds every intermediate in LDS (thread t owns element (t / 16, t % 16)) and runs expm.py's
+// algorithm start to finish: the 1-norm (column sums in row order), the branch and scaling,
+// the Pade polynomials in the reference's order (A2n = A2n @ A2 accumulation for m <= 9,
+// expm.py:37-47; the nested form for m = 13, :150-163), the solve of (V - U) R = V + U by
+// elimination with first-max partial pivoting (LAPACK getrf/getrs: multipliers times the
+// pivot's reciprocal, then the unit-lower and upper substitutions in order) and the s
+// squarings (matrix_power(r, 2**s)).
+constexpr int kSmallN = 16, kSL = kSmallN + 1;
+__constant__ double cB3[] = {120, 60, 12, 1};
+__constant__ double cB5[] = {30240, 15120, 3360, 420, 30, 1};
+__constant__ double cB7[] = {17297280, 8648640, 1995840, 277200, 25200, 1512, 56, 1};
+__constant__ double cB9[] = {17643225600.0, 8821612800.0, 2075673600.0, 302702400.0, 30270240.0,
+                             2162160.0,     110880.0,     3960.0,       90.0,        1.0};
+__constant__ double cB13[] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
+                              1187353796428800.0,  129060195264000.0,   10559470521600.0,
+                              670442572800.0,      33522128640.0,       1323241920.0,
+                              40840800.0,          960960.0,            16380.0,
+                              182.0,               1.0};
+__device__ __forceinline__ void sm_mul(const double (*X)[kSL], const double (*Y)[kSL],
+                                       double (*Z)[kSL], int n, int i, int j) {
+  if (i < n && j < n) {
+    double acc = 0.0;
+    for (int k = 0; k < n; ++k) acc = fma(X[i][k], Y[k][j], acc);
+    Z[i][j] = acc;
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) small_expm_kernel(int n, const double* __restrict__ Ab,
+                                                         double* __restrict__ outb) {
+#pragma clang fp contract(off)  // (products and sums rounded separately, like NumPy's)
+  __shared__ double A[kSmallN][kSL], P2[kSmallN][kSL], P4[kSmallN][kSL], P6[kSmallN][kSL],
+      U[kSmallN][kSL], V[kSmallN][kSL], T[kSmallN][kSL], W[kSmallN][kSL];
+  __shared__ double colsum[kSmallN];
+  __shared__ int piv_s;
+  const int t = threadIdx.x, i = t >> 4, j = t & 15;
+  const bool act = i < n && j < n;
+  const double* Ain = Ab + (int64_t)blockIdx.x * n * n;
+  if (act) A[i][j] = Ain[i * n + j];
+  __syncthreads();
+  if (t < n) {  // np.linalg.norm(A, 1): max over columns of the column's |.| sum, rows in order
+    double c = 0.0;
+    for (int r = 0; r < n; ++r) c += fabs(A[r][t]);
+    colsum[t] = c;
+  }
+  __syncthreads();
+  double norm = 0.0;
+  for (int c = 0; c < n; ++c) norm = fmax(norm, colsum[c]);
+  int m, sq = 0;
+  if (norm < 1.5e-2) m = 3;
+  else if (norm < 2.5e-1) m = 5;
+  else if (norm < 9.5e-1) m = 7;
+  else if (norm < 2.1) m = 9;
+  else {
+    m = 13;
+    const double v = ceil(log(norm / 5.4) / log(2.0));
+    sq = v > 0.0 ? (int)v : 0;
+  }
+  const double id = (i == j) ? 1.0 : 0.0;
+  if (m == 13) {
+    if (sq > 0 && act) A[i][j] = A[i][j] / ldexp(1.0, sq);  // A /= 2**s (exact)
+    __syncthreads();
+    const double* b = cB13;
+    sm_mul(A, A, P2, n, i, j);    // A2
+    sm_mul(P2, P2, P4, n, i, j);  // A4
+    sm_mul(P2, P4, P6, n, i, j);  // A6
+    if (act) T[i][j] = (b[13] * P6[i][j] + b[11] * P4[i][j]) + b[9] * P2[i][j];
+    __syncthreads();
+    sm_mul(P6, T, W, n, i, j);
+    if (act) T[i][j] = (((W[i][j] + b[7] * P6[i][j]) + b[5] * P4[i][j]) + b[3] * P2[i][j]) + b[1] * id;
+    __syncthreads();
+    sm_mul(A, T, U, n, i, j);  // U
+    if (act) T[i][j] = (b[12] * P6[i][j] + b[10] * P4[i][j]) + b[8] * P2[i][j];
+    __syncthreads();
+    sm_mul(P6, T, W, n, i, j);
+    if (act) V[i][j] = (((W[i][j] + b[6] * P6[i][j]) + b[4] * P4[i][j]) + b[2] * P2[i][j]) + b[0] * id;
+    __syncthreads();
+  } else {
+    const double* b = m == 3 ? cB3 : m == 5 ? cB5 : m == 7 ? cB7 : cB9;
+    // U = b1 I, V = b0 I; A2n = I; per i: A2n = A2n @ A2, U += b[2i+1] A2n, V += b[2i] A2n
+    sm_mul(A, A, P2, n, i, j);  // A2
+    double u = b[1] * id, v = b[0] * id;
+    if (act) T[i][j] = id;  // A2n
+    __syncthreads();
+    double (*cur)[kSL] = T;
+    double (*nxt)[kSL] = W;
+    for (int p = 1; p <= m / 2; ++p) {
+      sm_mul(cur, P2, nxt, n, i, j);
+      if (act) {
+        u += b[2 * p + 1] * nxt[i][j];
+        v += b[2 * p] * nxt[i][j];
+      }
+      double (*x)[kSL] = cur;
+      cur = nxt;
+      nxt = x;
+    }
+    if (act) {
+      P4[i][j] = u;
+      V[i][j] = v;
+    }
+    __syncthreads();
+    sm_mul(A, P4, U, n, i, j);  // U = A @ U
+  }
+  // (V - U) R = V + U: M in T, R in W
+  if (act) {
+    T[i][j] = V[i][j] - U[i][j];
+    W[i][j] = V[i][j] + U[i][j];
+  }
+  __syncthreads();
+  for (int c = 0; c < n; ++c) {
+    if (t == 0) {  // first row with the largest |M[r][c]|, r >= c (idamax)
+      int pr = c;
+      double best = fabs(T[c][c]);
+      for (int r = c + 1; r < n; ++r)
+        if (fabs(T[r][c]) > best) {
+          best = fabs(T[r][c]);
+          pr = r;
+        }
+      piv_s = pr;
+    }
+    __syncthreads();
+    const int pr = piv_s;
+    if (pr != c && t < 2 * kSmallN && (t & 15) < n) {  // swap rows c and pr of M and R
+      double (*X)[kSL] = t < kSmallN ? T : W;
+      const int col = t & 15;
+      const double x = X[c][col];
+      X[c][col] = X[pr][col];
+      X[pr][col] = x;
+    }
+    __syncthreads();
+    if (t > c && t < n) T[t][c] = T[t][c] * (1.0 / T[c][c]);  // multipliers
+    __syncthreads();
+    if (i > c && i < n && j < n) {
+      const double l = T[i][c];
+      if (j > c) T[i][j] = T[i][j] - l * T[c][j];
+      W[i][j] = W[i][j] - l * W[c][j];
+    }
+    __syncthreads();
+  }
+  for (int c = n - 1; c >= 0; --c) {  // upper substitution, column by column
+    if (t < n) W[c][t] = W[c][t] / T[c][c];
+    __syncthreads();
+    if (i < c && j < n) W[i][j] = W[i][j] - T[i][c] * W[c][j];
+    __syncthreads();
+  }
+  // s squarings: r^(2^s)
+  double (*cur)[kSL] = W;
+  double (*nxt)[kSL] = U;
+  for (int k = 0; k < sq; ++k) {
+    sm_mul(cur, cur, nxt, n, i, j);
+    double (*x)[kSL] = cur;
+    cur = nxt;
+    nxt = x;
+  }
+  if (act) outb[(int64_t)blockIdx.x * n * n + i * n + j] = cur[i][j];
+}
+
 hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipStream_t st) {
+  if (n >= 1 && n <= kSmallN && batch > 0) {
+    for (int64_t b0 = 0; b0 < batch; b0 += 65535)
+      hipLaunchKernelGGL(small_expm_kernel, dim3((unsigned)std::min<int64_t>(65535, batch - b0)),
+                         dim3(256), 0, st, n, A + b0 * n * n, out + b0 * n * n);
+    return hipGetLastError();
+  }
   return expm_blocktri_batched(n, 1, batch, A, out, st);
 }
 

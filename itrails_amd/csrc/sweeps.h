@@ -152,6 +152,36 @@ WaveVitGeometry wave_vit_geometry(int n);
 hipError_t launch_wave_vit(const WaveVitGeometry& g, int grid, const VitArgs& p,
                            hipStream_t st, int role = 0);
 
+// Viterbi for 72 < N <= 144 (prune_vit.hip): one block per wavefront, log a in the
+// workgroup's LDS, the bound-pruned step; outputs as VitArgs' (ckpt / stay / last_state)
+struct PruneVitArgs {
+  int n;                        // hidden states
+  int xr;                       // record stride of the checkpoint rows / flag words
+  int64_t nblocks;              // blocks of `order`
+  const int32_t* order;         // [nblocks] longest first
+  int* queue;                   // work counter, zero at launch
+  const int64_t* off;           // [plan blocks + 1]
+  const int64_t* tile_off;      // [plan blocks + 1]
+  const uint16_t* obs;          // [total]
+  const double* la;             // log a, n x n
+  const double* mj;             // [n] max_{i != j} log a_ij
+  const double* log_e;          // 625 x n
+  const double* lpie;           // log(pi E), 625 x n
+  double* ckpt;                 // [tiles x xr]
+  uint16_t* stay;               // [tiles x xr]
+  uint8_t* last_state;          // [plan blocks]
+  int prio_len;                 // blocks at least this long run at raised wave priority
+};
+struct PruneVitGeometry {
+  int waves;    // wavefronts (blocks at a time) per workgroup; 0: no layout for this n
+  int block;    // threads per workgroup
+  int sources;  // sources per scanning lane
+  size_t lds;   // dynamic LDS bytes
+};
+PruneVitGeometry prune_vit_geometry(int n);
+hipError_t launch_prune_vit(const PruneVitGeometry& g, int grid, const PruneVitArgs& p,
+                            hipStream_t st);
+
 // The reference's per-column matrices of one block (rows.hip): kind 0 = log alpha, 1 = log
 // beta, 2 = omega (+ prev when non-null); rows / prev are [T][n] / [T-1][n] float64
 struct RowArgs {

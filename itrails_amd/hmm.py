@@ -18,6 +18,9 @@ unavailable the calls raise.
 from __future__ import annotations
 
 import ctypes
+import hashlib
+import threading
+from collections import OrderedDict
 from typing import Iterable, List, Sequence
 
 import numpy as np
@@ -279,6 +282,109 @@ def _posteriors(model: Model, plan: Plan, obs: np.ndarray) -> np.ndarray:
 
 
 # ---------------------------------------------------------------------------------------
+# the wrappers' device objects, reused across calls: a caller scoring and then decoding one
+# alignment with one model (loglik_wrapper, then viterbi_wrapper / post_prob_wrapper) builds
+# the model tables, the Viterbi slot tables and the plan once.  Keys are the contents
+# (a, b, pi bytes; block offsets) and the current device, so a changed input is a new entry;
+# at most two of each are kept (evicted objects are freed when no caller holds them).
+# ---------------------------------------------------------------------------------------
+_CACHE_LOCK = threading.Lock()
+_MODELS: "OrderedDict" = OrderedDict()
+_PLANS: "OrderedDict" = OrderedDict()
+_CACHE_SIZE = 2
+
+
+def _device_index():
+    import torch
+    return torch.cuda.current_device()
+
+
+def _digest(*arrays):
+    h = hashlib.blake2b(digest_size=20)
+    for x in arrays:
+        x = np.ascontiguousarray(x)
+        h.update(f"{x.dtype.str}{x.shape}".encode())
+        h.update(memoryview(x).cast("B"))
+    return h.digest()
+
+
+def _cache_get(cache, key, make):
+    with _CACHE_LOCK:
+        obj = cache.get(key)
+        if obj is not None:
+            cache.move_to_end(key)
+            return obj
+    obj = make()
+    with _CACHE_LOCK:
+        cache[key] = obj
+        while len(cache) > _CACHE_SIZE:
+            cache.popitem(last=False)
+    return obj
+
+
+def _cached_model(a, b, pi, decode=False) -> Model:
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    pi = np.ascontiguousarray(pi, dtype=np.float64)
+    m = _cache_get(_MODELS, (_device_index(), _digest(a, b, pi)), lambda: Model(a, b, pi))
+    if decode and not getattr(m, "_prepared", False):
+        m.prepare_viterbi()
+        m._prepared = True
+    return m
+
+
+def _cached_plan(off) -> Plan:
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    return _cache_get(_PLANS, (_device_index(), _digest(off)), lambda: Plan(off))
+
+
+def clear_caches():
+    """Drop the wrappers' cached models and plans (their device memory is freed when no
+    caller holds them)."""
+    with _CACHE_LOCK:
+        _MODELS.clear()
+        _PLANS.clear()
+
+
+try:  # the V_lst scan in C (csrc/blocks_ext.c, built with the library)
+    from . import _blocks as _blocks_ext
+except ImportError:  # (argument marshalling only: the Python scan below does the same)
+    _blocks_ext = None
+
+
+def _lens_ptrs(V_lst):
+    """(lens, data pointers, offsets) of a V_lst of 1-D C-contiguous int64 arrays, or None
+    when some entry is not one (those inputs take the NumPy packing path)."""
+    nb = len(V_lst)
+    lens = np.empty(nb, dtype=np.int64)
+    ptrs = np.empty(nb, dtype=np.uintp)
+    if _blocks_ext is not None:
+        if not _blocks_ext.scan(V_lst, lens, ptrs):
+            return None
+    else:
+        for k, v in enumerate(V_lst):
+            if not (isinstance(v, np.ndarray) and v.dtype == np.int64 and v.ndim == 1 and
+                    v.flags.c_contiguous):
+                return None
+            lens[k] = v.shape[0]
+            ptrs[k] = v.ctypes.data
+    off = np.zeros(nb + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    return lens, ptrs, off
+
+
+def _check_data(rc):
+    if rc == _lib.ITR_EDATA:  # a symbol outside the alphabet: the reference's IndexError
+        raise IndexError(lib().itr_last_error().decode())
+    check(rc)
+
+
+def _split(arr, off):
+    o = off.tolist()
+    return [arr[i:j] for i, j in zip(o[:-1], o[1:])]
+
+
+# ---------------------------------------------------------------------------------------
 # reference layer: optimizer.py:145-377
 # ---------------------------------------------------------------------------------------
 def loglik_wrapper(a, b, pi, V_lst: Iterable[np.ndarray]) -> float:
@@ -287,9 +393,17 @@ def loglik_wrapper(a, b, pi, V_lst: Iterable[np.ndarray]) -> float:
     V_lst = list(V_lst)
     if not V_lst:
         return 0
-    obs, off = concat_blocks(V_lst)
-    model, plan = Model(a, b, pi), Plan(off)
-    ll = block_logliks(model, plan, obs)
+    lp = _lens_ptrs(V_lst)
+    if lp is not None:  # read_data.py's blocks: packed into pinned memory by the library
+        lens, ptrs, off = lp
+        model, plan = _cached_model(a, b, pi), _cached_plan(off)
+        ll = np.empty(len(V_lst))
+        _check_data(lib().itr_forward_loglik_blocks(model.handle, plan.handle, ptr(ptrs),
+                                                    ptr(lens), len(V_lst), ptr(ll)))
+    else:
+        obs, off = concat_blocks(V_lst)
+        model, plan = _cached_model(a, b, pi), _cached_plan(off)
+        ll = block_logliks(model, plan, obs)
     acc = 0
     for v in ll.tolist():
         acc += v
@@ -310,12 +424,24 @@ def forward_loglik(a, b, pi, V, order=None) -> float:
 def viterbi_wrapper(a, b, pi, V_lst: Iterable[np.ndarray]) -> List[np.ndarray]:
     """Viterbi path per block as float64 arrays (optimizer.py:357-377, 336-354)."""
     V_lst = list(V_lst)
+    if not V_lst:
+        return []
+    lp = _lens_ptrs(V_lst)
+    if lp is not None:
+        lens, ptrs, off = lp
+        if off[-1] == 0:
+            return [np.zeros(0) for _ in V_lst]
+        model, plan = _cached_model(a, b, pi, decode=True), _cached_plan(off)
+        path = np.empty(int(off[-1]))
+        _check_data(lib().itr_viterbi_blocks(model.handle, plan.handle, ptr(ptrs), ptr(lens),
+                                             len(V_lst), ptr(path)))
+        return _split(path, off)
     obs, off = concat_blocks(V_lst)
     if off[-1] == 0:
         return [np.zeros(0) for _ in V_lst]
-    model, plan = Model(a, b, pi), Plan(off)
+    model, plan = _cached_model(a, b, pi, decode=True), _cached_plan(off)
     path = _paths(model, plan, obs).astype(np.float64)
-    return [path[off[k]:off[k + 1]] for k in range(len(V_lst))]
+    return _split(path, off)
 
 
 def post_prob_wrapper(a, b, pi, V_lst: Iterable[np.ndarray]) -> List[np.ndarray]:
@@ -325,9 +451,9 @@ def post_prob_wrapper(a, b, pi, V_lst: Iterable[np.ndarray]) -> List[np.ndarray]
     n = np.asarray(a).shape[0]
     if off[-1] == 0:
         return [np.zeros((0, n)) for _ in V_lst]
-    model, plan = Model(a, b, pi), Plan(off)
+    model, plan = _cached_model(a, b, pi), _cached_plan(off)
     post = _posteriors(model, plan, obs)
-    return [post[off[k]:off[k + 1]] for k in range(len(V_lst))]
+    return _split(post, off)
 
 
 def post_prob(a, b, pi, V, order=None) -> np.ndarray:

@@ -77,3 +77,22 @@ def test_pack_symbols_matches_numpy_and_rejects_bad_symbols():
             hmm.concat_blocks(W)
     e, eo = hmm.concat_blocks([np.zeros(0, dtype=np.int64)] * 3)
     assert e.size == 0 and np.array_equal(eo, [0, 0, 0, 0])
+
+
+def test_vlst_scan_extension():
+    """The V_lst scan of the host-block entry points (csrc/blocks_ext.c): lengths and data
+    pointers of 1-D C-contiguous int64 arrays; anything else (other dtypes, 2-D, strided,
+    byte-swapped, lists) takes the NumPy packing path (None)."""
+    import numpy as np
+
+    from itrails_amd import hmm
+
+    assert hmm._blocks_ext is not None  # built with the library (itrails_amd/build.py)
+    V = [np.arange(k % 37, dtype=np.int64) for k in range(3000)]
+    lens, ptrs, off = hmm._lens_ptrs(V)
+    assert np.array_equal(lens, [len(v) for v in V])
+    assert np.array_equal(ptrs, [v.ctypes.data for v in V])
+    assert np.array_equal(off, np.concatenate([[0], np.cumsum(lens)]))
+    for bad in (np.zeros(3, np.int32), np.zeros((2, 2), np.int64), np.zeros(6, np.int64)[::2],
+                np.zeros(3, ">i8"), [1, 2]):
+        assert hmm._lens_ptrs(V[:5] + [bad]) is None

@@ -292,3 +292,39 @@ def test_few_long_blocks_forward_viterbi(gpu, n):
     np.testing.assert_array_equal(p2, p1)
     np.testing.assert_array_equal(p2, O.viterbi(t, obs, off))
     np.testing.assert_allclose(ll2, O.forward_loglik(t, obs, off), rtol=RTOL, atol=0)
+
+
+def test_wrappers_host_blocks_paths(gpu):
+    """loglik_wrapper / viterbi_wrapper on int64 blocks (the pinned host-block entry points,
+    itr_forward_loglik_blocks / itr_viterbi_blocks) against the same calls on int32 blocks
+    (the NumPy packing path) and the goldens: identical results; a symbol outside the
+    alphabet raises IndexError naming its block and column; a model or layout change after a
+    cached call is a new cache entry."""
+    g = golden("sweep_syn70.npz")
+    a, b, pi, obs, off = g["a"], g["b"], g["pi"], g["obs"], g["off"]
+    V64 = [obs[off[k]:off[k + 1]].astype(np.int64) for k in range(len(off) - 1)]
+    V32 = [v.astype(np.int32) for v in V64]
+    for _ in range(2):  # second round: cached model and plan
+        assert hmm.loglik_wrapper(a, b, pi, V64) == hmm.loglik_wrapper(a, b, pi, V32)
+        p64, p32 = hmm.viterbi_wrapper(a, b, pi, V64), hmm.viterbi_wrapper(a, b, pi, V32)
+        assert all(x.dtype == np.float64 for x in p64)
+        np.testing.assert_array_equal(np.concatenate(p64), np.concatenate(p32))
+        np.testing.assert_array_equal(np.concatenate(p64), g["path"].astype(np.float64))
+    W = [v.copy() for v in V64]
+    W[2][7] = 625
+    with pytest.raises(IndexError, match="block 2, column 7"):
+        hmm.loglik_wrapper(a, b, pi, W)
+    with pytest.raises(IndexError, match="block 2, column 7"):
+        hmm.viterbi_wrapper(a, b, pi, W)
+    # another model with the same layout, and the same model on a sub-layout
+    a2 = np.ascontiguousarray(a[::-1, ::-1])
+    b2, pi2 = np.ascontiguousarray(b[::-1]), np.ascontiguousarray(pi[::-1])
+    t2 = build_tables(a2, b2, pi2)
+    np.testing.assert_array_equal(np.concatenate(hmm.viterbi_wrapper(a2, b2, pi2, V64)),
+                                  O.viterbi(t2, obs, off).astype(np.float64))
+    sub = V64[1:3]
+    so = np.concatenate(sub).astype(np.uint16)
+    soff = np.concatenate([[0], np.cumsum([len(v) for v in sub])])
+    ll = hmm.loglik_wrapper(a, b, pi, sub)
+    ref = O.forward_loglik(build_tables(a, b, pi), so, soff)
+    assert abs(ll - (ref[0] + ref[1])) <= 1e-9 * abs(ll)
