@@ -1683,10 +1683,17 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
                                             p->d_svec, p->d_sK, fwd_loglik, st));
   } else if (!few) {
     const itr::PruneVitGeometry pg = itr::prune_vit_geometry(m->n);
-    // (few blocks: their lone step latency bounds the call — the 9-wave layout's is lower)
-    bool prune = pg.waves > 0 && m->MJ && p->nblocks > 2 * cus;
+    // Only where it measured faster (profiles/r5h_pv_lab.txt): N = 133 on short blocks
+    // (mean 300: 5.4 vs 8.2 ms per 3 Mbp).  Its scans read log a from LDS, so a column costs
+    // LDS bandwidth in proportion to its failing targets: 6 % of them fail on short blocks,
+    // 15 % on the config-2 layout (71 vs 25 ms) and 46 % deep inside long blocks (3.2 us per
+    // lone column vs 0.64 on the 9-wave layout); at N = 95 the 9-wave layout wins throughout.
+    const int64_t mean_len = p->total / std::max<int64_t>(1, p->nblocks);
+    bool prune = pg.waves > 0 && m->MJ && m->n > 128 && mean_len <= 400 &&
+                 p->nblocks > 2 * cus;
 #ifdef ITR_EXPERIMENT
     if (getenv("ITR_NO_PRUNE_VIT")) prune = false;
+    if (getenv("ITR_PV_FORCE")) prune = pg.waves > 0 && m->MJ;
 #endif
     if (prune) {
       // one block per wavefront, log a in LDS, the bound-pruned step (prune_vit.hip)
@@ -1713,7 +1720,24 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       const int64_t grid = std::min<int64_t>(cus, (p->nblocks + pg.waves - 1) / pg.waves);
       std::optional<Scope> sc;
       if (!fwd_loglik) sc.emplace("viterbi", st);
+#ifdef ITR_EXPERIMENT
+      static unsigned long long* d_pvdiag = nullptr;
+      if (getenv("ITR_PV_DIAG")) {
+        if (!d_pvdiag) HIP_TRY(hipMalloc(&d_pvdiag, 4 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(d_pvdiag, 0, 4 * sizeof(unsigned long long), st));
+        v.diag = d_pvdiag;
+      }
+#endif
       HIP_TRY(itr::launch_prune_vit(pg, (int)grid, v, st));
+#ifdef ITR_EXPERIMENT
+      if (v.diag) {
+        unsigned long long h[3];
+        HIP_TRY(hipMemcpyAsync(h, d_pvdiag, sizeof h, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        fprintf(stderr, "prune_vit: %llu steps, %.2f failing targets and %.2f passes per step\n",
+                h[0], (double)h[1] / std::max(1ull, h[0]), (double)h[2] / std::max(1ull, h[0]));
+      }
+#endif
     } else {
       if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
     }

@@ -124,6 +124,9 @@ __device__ __forceinline__ void pv_block(const PruneVitArgs& p, const double* la
     if (jv[g]) p.ckpt[tk0 * xr + jt[g]] = w[g];
   wait_vmem_all();
   const int q = l & (kPvQ - 1), k8 = l >> 3;
+#ifdef ITR_EXPERIMENT
+  unsigned long long dg_f = 0, dg_p = 0;
+#endif
   for (int t = 1; t < T; ++t) {
     const int sub = t & (VIT_TILE - 1);
     if ((t & 63) == 0) {  // next 64 symbols (the lanes' register already holds them)
@@ -165,6 +168,10 @@ __device__ __forceinline__ void pv_block(const PruneVitArgs& p, const double* la
       base += __builtin_popcountll(fb[g]);
     }
     const int nf = uni(base);
+#ifdef ITR_EXPERIMENT
+    dg_f += nf;
+    dg_p += (nf + 7) / 8;
+#endif
     wave_lds_sync();
     // scans of the failing targets, eight per pass
     for (int k0 = 0; k0 < nf; k0 += 8) {
@@ -229,6 +236,13 @@ __device__ __forceinline__ void pv_block(const PruneVitArgs& p, const double* la
     }
   wave_first_max(bv, bj);
   if (l == 0) p.last_state[blk] = (uint8_t)bj;
+#ifdef ITR_EXPERIMENT
+  if (p.diag && l == 0) {
+    atomicAdd(&p.diag[0], (unsigned long long)(T - 1));
+    atomicAdd(&p.diag[1], dg_f);
+    atomicAdd(&p.diag[2], dg_p);
+  }
+#endif
   if (urgent) __builtin_amdgcn_s_setprio(0);
   wave_lds_sync();
 }
@@ -269,6 +283,8 @@ size_t pv_lds(int n, int waves) {
 PruneVitGeometry prune_vit_geometry(int n) {
   PruneVitGeometry g{};
   g.waves = 0;
+  // (N <= 72: the per-wave layouts of wave_tasks.h; this kernel on the (5,5) bulk measured
+  // 13.2 vs 6.1 ms per itr_viterbi call, profiles/r5i_pv_bulk70_ab.txt)
   if (n <= 72 || n > kPvNmax) return g;
   // as many waves (blocks) per CU as the LDS holds beside the matrix, at most 16
   int waves = 16;

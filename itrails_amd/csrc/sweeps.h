@@ -171,6 +171,7 @@ struct PruneVitArgs {
   uint16_t* stay;               // [tiles x xr]
   uint8_t* last_state;          // [plan blocks]
   int prio_len;                 // blocks at least this long run at raised wave priority
+  unsigned long long* diag;     // experiment build only: {columns, failing targets, passes}
 };
 struct PruneVitGeometry {
   int waves;    // wavefronts (blocks at a time) per workgroup; 0: no layout for this n

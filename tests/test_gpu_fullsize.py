@@ -331,3 +331,22 @@ def test_full_size_intro95_every_block(gpu):
     assert _posterior_every_block(t, obs[:off[nb]], off[:nb + 1], post) == off[nb]
     del post, d_obs
     torch.cuda.empty_cache()
+
+
+def test_short_blocks_133_pruned_viterbi(gpu):
+    """The bound-pruned Viterbi (prune_vit.hip: one block per wavefront, log a in LDS), which
+    itr_viterbi / itr_forward_viterbi take at N = 133 for many short blocks: 2 Mbp of the
+    (7,7) model in geometric blocks of mean 300 columns, every path against the CPU
+    restatement, the log-likelihoods of the combined call 1e-8."""
+    import torch
+    g = golden("model_kat_7_7.npz")
+    a, b, pi = g["a"], g["b"], g["pi"]
+    lengths = block_lengths(np.random.default_rng(1), 2_000_000, 300.0)
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=778)
+    assert len(lengths) > 2 * 256 and off[-1] / len(lengths) <= 400  # (the kernel's regime)
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).cuda()
+    path = hmm.viterbi_device(model, plan, d_obs).cpu().numpy()
+    ll, path2 = hmm.forward_viterbi_device(model, plan, d_obs)
+    assert np.array_equal(path2.cpu().numpy(), path)
+    _check_all_blocks(build_tables(a, b, pi), obs, off, ll.cpu().numpy(), path)
