@@ -1914,10 +1914,14 @@ struct HostIO {
   size_t pin_cap = 0;
   void* dbuf = nullptr;
   size_t dcap = 0;
+  hipStream_t st = nullptr;  // the calls' own non-blocking stream (no legacy-stream syncs)
   void release() {
+    if (st) (void)hipStreamSynchronize(st);
     if (pin) (void)hipHostFree(pin);
     if (dbuf) (void)hipFree(dbuf);
+    if (st) (void)hipStreamDestroy(st);
     pin = dbuf = nullptr;
+    st = nullptr;
     pin_cap = dcap = 0;
     device = -1;
   }
@@ -1928,6 +1932,7 @@ struct HostIO {
       release();
       device = dev;
     }
+    if (!st) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     if (pin_bytes > pin_cap) {
       if (pin) (void)hipHostFree(pin);
       pin = nullptr;
@@ -2313,14 +2318,16 @@ namespace {
 // V_lst -> uint16 columns at the given offsets: the blocks are split into contiguous ranges
 // of about equal column count, one per thread; each thread converts and range-checks its
 // own blocks, and the first bad symbol (lowest block) is reported.
+// Blocks [0, n_blocks) of the given arrays (block_off absolute: obs + block_off[k] is block
+// k's first column; k_base = the first block's index in messages).
 int pack_blocks(const int64_t* const* blocks, const int64_t* lens, const int64_t* block_off,
-                int64_t n_blocks, uint16_t* obs) {
-  const int64_t total = block_off[n_blocks];
+                int64_t n_blocks, uint16_t* obs, int64_t k_base = 0) {
+  const int64_t c_begin = block_off[0], total = block_off[n_blocks] - c_begin;
   if (total == 0) return 0;
   const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, total >> 18));
   std::vector<int64_t> bad(nt, -1), bad_col(nt, -1);
   parallel_for(nt, [&](int w) {
-    const int64_t lo_col = total * w / nt, hi_col = total * (w + 1) / nt;
+    const int64_t lo_col = c_begin + total * w / nt, hi_col = c_begin + total * (w + 1) / nt;
     // blocks whose first column falls in [lo_col, hi_col)
     int64_t k = std::lower_bound(block_off, block_off + n_blocks, lo_col) - block_off;
     for (; k < n_blocks && block_off[k] < hi_col; ++k) {
@@ -2346,7 +2353,7 @@ int pack_blocks(const int64_t* const* blocks, const int64_t* lens, const int64_t
     if (bad[w] >= 0)
       return fail(ITR_EDATA, "observed symbol %lld (block %lld, column %lld) outside the "
                   "625-letter alphabet", (long long)blocks[bad[w]][bad_col[w]],
-                  (long long)bad[w], (long long)bad_col[w]);
+                  (long long)(k_base + bad[w]), (long long)bad_col[w]);
   return 0;
 }
 
@@ -2369,11 +2376,21 @@ int upload_blocks(itr_plan_t p, const int64_t* const* blocks, const int64_t* len
   const size_t ob16 = (ob + 255) & ~(size_t)255;
   if (int e = g_hio.reserve(std::max(ob, (size_t)p->total), ob16 + extra_dev)) return e;
   uint16_t* h = (uint16_t*)g_hio.pin;
-  if (int e = pack_blocks(blocks, lens, p->h_off.data(), n_blocks, h)) return e;
   *d_obs = (uint16_t*)g_hio.dbuf;
-  if (p->total)
-    HIP_TRY(hipMemcpyAsync(*d_obs, h, p->total * sizeof(uint16_t), hipMemcpyHostToDevice,
-                           nullptr));
+  // two halves (by blocks): the first half's copy runs while the second is packed
+  const int64_t kh = std::lower_bound(p->h_off.begin(), p->h_off.end() - 1, p->total / 2) -
+                     p->h_off.begin();
+  const int64_t cuts[3] = {0, std::min<int64_t>(kh, n_blocks), n_blocks};
+  for (int part = 0; part < 2; ++part) {
+    const int64_t k0 = cuts[part], k1 = cuts[part + 1];
+    if (k1 <= k0) continue;
+    if (int e = pack_blocks(blocks + k0, lens + k0, p->h_off.data() + k0, k1 - k0, h, k0))
+      return e;
+    const int64_t c0 = p->h_off[k0], c1 = p->h_off[k1];
+    if (c1 > c0)
+      HIP_TRY(hipMemcpyAsync(*d_obs + c0, h + c0, (c1 - c0) * sizeof(uint16_t),
+                             hipMemcpyHostToDevice, g_hio.st));
+  }
   return 0;
 }
 size_t dev_tail(itr_plan_t p) {  // first byte after the observations in g_hio.dbuf
@@ -2428,9 +2445,11 @@ int itr_forward_loglik_blocks(itr_model_t m, itr_plan_t p, const int64_t* const*
   clk.lap("loglik: pack+h2d");
   if (p->nblocks == 0) return 0;
   double* d_ll = (double*)((char*)g_hio.dbuf + tail);
-  if (int e = itr_forward_loglik(m, p, d_obs, d_ll, nullptr)) return e;
+  if (int e = itr_forward_loglik(m, p, d_obs, d_ll, g_hio.st)) return e;
   clk.lap("sweep");
-  HIP_TRY(hipMemcpy(h_ll, d_ll, p->nblocks * sizeof(double), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpyAsync(h_ll, d_ll, p->nblocks * sizeof(double), hipMemcpyDeviceToHost,
+                         g_hio.st));
+  HIP_TRY(hipStreamSynchronize(g_hio.st));
   clk.lap("d2h");
   clk.end();
   return 0;
@@ -2448,15 +2467,23 @@ int itr_viterbi_blocks(itr_model_t m, itr_plan_t p, const int64_t* const* blocks
   clk.lap("viterbi: pack+h2d");
   if (p->total == 0) return 0;
   uint8_t* d_path = (uint8_t*)g_hio.dbuf + tail;
-  if (int e = itr_viterbi(m, p, d_obs, d_path, nullptr)) return e;
+  if (int e = itr_viterbi(m, p, d_obs, d_path, g_hio.st)) return e;
+  const int64_t total = p->total;
+  const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, total >> 18));
+  // while the device sweeps: host threads map the output's pages (one write per 4 KiB), so
+  // the widening below does not page-fault its way through a fresh 8-bytes-per-column array
+  if (!clk.on)
+    parallel_for(nt, [&](int w) {
+      const int64_t lo = total * w / nt, hi = total * (w + 1) / nt;
+      for (int64_t c = lo; c < hi; c += 512) h_path[c] = 0.0;
+    });
   clk.lap("sweep");
   // the states back through the pinned buffer (the observations' upload finished before the
   // sweep on this stream), widened to float64 (the reference's path dtype) by host threads
   uint8_t* h = (uint8_t*)g_hio.pin;
-  HIP_TRY(hipMemcpy(h, d_path, p->total, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpyAsync(h, d_path, p->total, hipMemcpyDeviceToHost, g_hio.st));
+  HIP_TRY(hipStreamSynchronize(g_hio.st));
   clk.lap("d2h");
-  const int64_t total = p->total;
-  const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, total >> 18));
   parallel_for(nt, [&](int w) {
     const int64_t lo = total * w / nt, hi = total * (w + 1) / nt;
     for (int64_t c = lo; c < hi; ++c) h_path[c] = (double)h[c];

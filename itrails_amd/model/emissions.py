@@ -167,19 +167,28 @@ def jc69_rate(mu: float) -> np.ndarray:
     return np.full((4, 4), mu / 4) - np.diag([mu, mu, mu, mu])
 
 
-def branch_generator(ts, mus) -> np.ndarray:
-    """sum_k t_k Q_k (p_b_given_a, get_emission_prob_mat.py:22-44), exponentiated later.
-    Every Q_k = jc69_rate(mu_k) has one off-diagonal value mu/4 and one diagonal value
-    mu/4 - mu, so the elementwise sum is two scalar sums in the same order (bit-equal)."""
+def branch_generator(ts, mus) -> tuple:
+    """sum_k t_k Q_k (p_b_given_a, get_emission_prob_mat.py:22-44), exponentiated later, as
+    its two distinct entries (off-diagonal, diagonal): every Q_k = jc69_rate(mu_k) has one
+    off-diagonal value mu/4 and one diagonal value mu/4 - mu, so the elementwise sum is two
+    scalar sums in the same order (bit-equal); generator_matrices expands them."""
     off = 0.0
     dg = 0.0
     for t, mu in zip(ts, mus):
         q = mu / 4
         off = off + t * q
         dg = dg + t * (q - mu)
-    mat = np.full((4, 4), off)
-    np.fill_diagonal(mat, dg)
-    return mat
+    return (off, dg)
+
+
+def generator_matrices(gens) -> np.ndarray:
+    """(G, 4, 4) matrices of branch_generator pairs: off-diagonal entries `off`, diagonal `dg`."""
+    g = np.asarray(gens, dtype=np.float64).reshape(-1, 2)
+    out = np.empty((g.shape[0], 4, 4))
+    out[:] = g[:, 0, None, None]
+    d = np.arange(4)
+    out[:, d, d] = g[:, 1, None]
+    return out
 
 
 # ---------------------------------------------------------------------------------------
@@ -262,7 +271,7 @@ def emission_rows(specs, la=None) -> Tuple[List[tuple], np.ndarray]:
             if m is not None:
                 where.append((s, g))
                 gens.append(m)
-    P = la.expm(gens)
+    P = la.expm(list(generator_matrices(gens)))
     tab = np.zeros((len(specs), ET_STRIDE))
     slot = [ET_A, ET_B, ET_C, ET_D, ET_AB]
     for (s, g), m in zip(where, P):

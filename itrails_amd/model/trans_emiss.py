@@ -20,6 +20,25 @@ OBSERVED_NAMES = {i: _NT[i >> 6] + _NT[(i >> 4) & 3] + _NT[(i >> 2) & 3] + _NT[i
                   for i in range(256)}
 
 
+_PAIR_INDEX: dict = {}
+
+
+def _pair_index(n_int_AB, n_int_ABC, hidden, J):
+    """Row / column of every joint-probability key (in J's order) in the sorted hidden-state
+    order.  J's keys come in the same order at every rebuild of one model size (the chain's
+    planned enumeration), so the index arrays are built once per size and reused while the
+    states and the keys' count and ends match."""
+    keys = list(J.keys())
+    k = (n_int_AB, n_int_ABC)
+    c = _PAIR_INDEX.get(k)
+    if c is None or c[0] != hidden or c[1] != keys:
+        index = {s: i for i, s in enumerate(hidden)}
+        r = np.fromiter((index[tuple(a)] for a, _ in keys), dtype=np.int64, count=len(keys))
+        q = np.fromiter((index[tuple(d)] for _, d in keys), dtype=np.int64, count=len(keys))
+        c = _PAIR_INDEX[k] = (list(hidden), keys, r, q)
+    return c[2], c[3]
+
+
 def trans_emiss_calc(t_A, t_B, t_C, t_2, t_upper, t_out, N_AB, N_ABC, r, n_int_AB,
                      n_int_ABC, cut_AB="standard", cut_ABC="standard", la=None):
     """-> (a, b, pi, hidden_names, observed_names), the reference's return tuple."""
@@ -60,11 +79,10 @@ def trans_emiss_calc(t_A, t_B, t_C, t_2, t_upper, t_out, N_AB, N_ABC, r, n_int_A
     order = sorted(range(len(states)), key=lambda i: states[i])
     hidden = [states[i] for i in order]
     b = rows[order]
-    index = {s: k for k, s in enumerate(hidden)}
     n = len(hidden)
+    rows_idx, cols_idx = _pair_index(n_int_AB, n_int_ABC, hidden, J)
     T = np.zeros((n, n))
-    for (src, dst), p in J.items():
-        T[index[tuple(src)], index[tuple(dst)]] = p
+    T[rows_idx, cols_idx] = np.fromiter(J.values(), dtype=np.float64, count=len(J))
     pi = T.sum(axis=1)
     a = T / pi[:, None]
     return a, b, pi, dict(enumerate(hidden)), dict(OBSERVED_NAMES)
