@@ -86,41 +86,50 @@ struct MLds {
   static constexpr size_t bytes = kf_off + (size_t)GB * 4 * 4;
 };
 
-// y[gb] = x_gb(row ra, sources kk NK ..) @ B for the GB groups of a task: the A operands
-// (four per group) are read one k-step ahead and the groups' MFMAs interleaved, so an LDS
-// round trip hides under 4 GB MFMAs.  The empty asm keeps the compiler from hoisting every
-// read to the top (their registers would spill the matrix slice) or from serialising them
-// into one register quad (a full LDS round trip per two MFMAs: the round-2 code at N = 133)
+// y[gb] = x_gb(row ra, sources kk NK ..) @ B for the GB groups of a task.  The A operands
+// (two per ds_read_b128) stream through a ring of D reads in flight per group, refilled
+// behind the MFMAs that consume them: an LDS round trip (~100 cycles) then hides under 2 D GB
+// MFMAs (16 cycles each).  With one read ahead (the round-4 form) every pair of MFMAs waited
+// for its operands (lgkmcnt(1) before each pair in the ISA).  The empty asm keeps the
+// compiler from hoisting every read to the top (their registers would spill the matrix
+// slice) or from serialising them.  Same MFMAs, same accumulators, same order: bit-identical.
 template <int NK, int GB>
 __device__ __forceinline__ void mfma_chain(const double* const (&xs)[GB], const double (&B)[NK],
                                            double (&y)[GB]) {
-  constexpr int W = 2;  // A operands per group per k-step (one ds_read_b128)
+  constexpr int W = 2;                 // A operands per group per read (one ds_read_b128)
+  constexpr int NQ = (NK + W - 1) / W; // reads per group
+  constexpr int D = NQ < 4 ? NQ : 4;   // reads in flight per group
   // four accumulator chains per group (source s into chain s % 4: the 52-cycle dependent
   // MFMA latency under 4 x 16 issue cycles), summed as (0 + 1) + (2 + 3)
-  double acc[GB][4], cur[GB][W], nxt[GB][W];
+  double acc[GB][4], ring[GB][D][W];
 #pragma unroll
   for (int gb = 0; gb < GB; ++gb) {
     acc[gb][0] = acc[gb][1] = acc[gb][2] = acc[gb][3] = 0.0;
 #pragma unroll
-    for (int u = 0; u < W; ++u) cur[gb][u] = u < NK ? xs[gb][u] : 0.0;
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int u = 0; u < W; ++u) ring[gb][d][u] = d * W + u < NK ? xs[gb][d * W + u] : 0.0;
   }
+  asm volatile("" ::: "memory");
 #pragma unroll
-  for (int q = 0; q < NK; q += W) {
-    if (q + W < NK) {
-#pragma unroll
-      for (int gb = 0; gb < GB; ++gb)
-#pragma unroll
-        for (int u = 0; u < W; ++u) nxt[gb][u] = q + W + u < NK ? xs[gb][q + W + u] : 0.0;
-    }
+  for (int qi = 0; qi < NQ; ++qi) {
+    const int slot = qi % D;
 #pragma unroll
     for (int u = 0; u < W; ++u)
 #pragma unroll
+      for (int gb = 0; gb < GB; ++gb) {
+        const int k = qi * W + u;
+        if (k < NK) acc[gb][k & 3] = mfma4(ring[gb][slot][u], B[k], acc[gb][k & 3]);
+      }
+    if (qi + D < NQ) {
+#pragma unroll
       for (int gb = 0; gb < GB; ++gb)
-        if (q + u < NK) acc[gb][(q + u) & 3] = mfma4(cur[gb][u], B[q + u], acc[gb][(q + u) & 3]);
 #pragma unroll
-    for (int gb = 0; gb < GB; ++gb)
-#pragma unroll
-      for (int u = 0; u < W; ++u) cur[gb][u] = nxt[gb][u];
+        for (int u = 0; u < W; ++u) {
+          const int k = (qi + D) * W + u;
+          ring[gb][slot][u] = k < NK ? xs[gb][k] : 0.0;
+        }
+    }
     asm volatile("" ::: "memory");
   }
 #pragma unroll
