@@ -188,13 +188,7 @@ int partition(int reserve, int reserve2, Partition** out, bool masked = true) {
   // side of the partition.
   const int X = (cus % 8 == 0) ? 8 : 1, L = cus / X;
   std::vector<char> in(cus, 0);  // 1: lng, 2: lng2
-  int mode = 0;
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_MASK_MODE")) mode = atoi(getenv("ITR_MASK_MODE"));
-#endif
-  if (mode == 1) {  // round-2 pattern: every (cus / reserve)-th logical bit
-    for (int k = 0; k < reserve; ++k) in[(int)((int64_t)k * cus / reserve)] = 1;
-  } else {
+  {
     // within an XCC, CU index k belongs to shader engine k % 4 (cumask2.hip: local k ->
     // se k % 4); the dispatcher deals a launch's workgroups to the shader engines in turn, so
     // each set takes the same number of CUs from every engine (a one-workgroup-per-CU launch
@@ -217,12 +211,9 @@ int partition(int reserve, int reserve2, Partition** out, bool masked = true) {
   }
   for (int c = 0; c < cus; ++c)
     (in[c] == 1 ? ml : in[c] == 2 ? ml2 : mb)[c / 32] |= 1u << (c % 32);
-  if (mode == 3)  // the bulk may share the long Viterbi blocks' CUs (one workgroup beside each)
-    for (int c = 0; c < cus; ++c)
-      if (in[c] == 1) mb[c / 32] |= 1u << (c % 32);
   if (reserve <= 0) std::fill(ml.begin(), ml.end(), 0xFFFFFFFFu);  // (lng unused)
   if (reserve2 <= 0) ml2 = ml;
-  if (mode == 2 || !masked) {  // no masks
+  if (!masked) {  // no masks
     std::fill(ml.begin(), ml.end(), 0xFFFFFFFFu);
     std::fill(ml2.begin(), ml2.end(), 0xFFFFFFFFu);
     std::fill(mb.begin(), mb.end(), 0xFFFFFFFFu);
@@ -1072,7 +1063,11 @@ int plan_create_impl(const int64_t* off, int64_t nblocks, double split_frac,
     std::vector<int64_t> gidx(ng);
     std::iota(gidx.begin(), gidx.end(), 0);
     std::stable_sort(gidx.begin(), gidx.end(), [&](int64_t x, int64_t y) { return gsteps[x] > gsteps[y]; });
-    const double cf = kMixFwd, cv = kMixVit;
+    double cf = kMixFwd, cv = kMixVit;
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_MIX_FWD")) cf = atof(getenv("ITR_MIX_FWD"));
+    if (getenv("ITR_MIX_VIT")) cv = atof(getenv("ITR_MIX_VIT"));
+#endif
     int64_t gi = 0, vi = p->vit_nlong;
     const int64_t nprio = kMixPrio;
     while (gi < ng || vi < nblocks) {
@@ -1466,10 +1461,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   const int64_t rv0 = nlong_c > 0 ? std::max(1, p->vit_reserve) : 0;
   // whole XCC sets: a mask that leaves an XCC without a reserved CU does not mask it at all
   const int X = (cus % 8 == 0) ? 8 : 1;
-  int Xr = X;  // rounding unit of the reserved sets
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_SE_ROUND")) Xr = 4 * X;  // one CU per shader engine
-#endif
+  const int Xr = X;  // rounding unit of the reserved sets
   const int rvr = (int)std::min<int64_t>((rv0 + Xr - 1) / Xr * Xr, cus / 2);
   const int rfr = (int)std::min<int64_t>((rf0 + Xr - 1) / Xr * Xr, cus / 4);
   const int reserve_cus = rvr + rfr;

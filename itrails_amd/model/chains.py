@@ -96,36 +96,72 @@ def _branch_rows_abc(side, step):
 
 def run_chain_ab(Q, times, masks, probs: Dict, n_int, la) -> Dict:
     """run_markov_chain_AB.py:105-271: two-species chain over the n_int AB intervals (every
-    interval's propagator expm(Q dt) requested as one batch up front)."""
+    interval's propagator expm(Q dt) requested as one batch up front).
+
+    Within a step every product reads a step-start row: a path writes only new keys or its
+    own (keys of the step's other paths are skipped), and after its reads.  So a step is one
+    batched product over its (path, key) updates, applied in the reference's write order —
+    planned once per (n_int, starting keys) from the key structure alone (_plan_ab)."""
     Es = la.expm([Q * times[step] for step in range(n_int)])
+    keys0 = list(probs.keys())
+    pk = (n_int, tuple(keys0), id(masks))
+    plan = _AB_PLANS.get(pk)
+    if plan is None:
+        plan = _AB_PLANS[pk] = _plan_ab(masks, keys0, n_int)
+    V = np.concatenate([np.asarray(probs[k], dtype=np.float64).reshape(1, -1) for k in keys0])
+    for step, (pidx, ms, me, take_old, take_upd) in enumerate(plan.steps):
+        A = V[pidx]
+        if step > 0:
+            A = A * ms  # (pm * ms) @ E * me, run_markov_chain_AB.py:262-270
+        R = (A @ Es[step]) * me  # step 0: (pm @ E) * me, run_markov_chain_AB.py:9-12
+        Vn = np.empty((len(take_old), V.shape[1]))
+        old = take_old >= 0
+        Vn[old] = V[take_old[old]]
+        Vn[~old] = R[take_upd[~old]]
+        V = Vn
+    return {k: V[i:i + 1] for i, k in enumerate(plan.keys)}
+
+
+_AB_PLANS: Dict = {}
+
+
+class _ABPlan:
+    __slots__ = ("steps", "keys")
+
+
+def _plan_ab(masks, keys0, n_int) -> _ABPlan:
+    """The two-species chain's structure: per step the updates (source row, start mask,
+    end mask) of every (path, candidate key) the reference evaluates, and the resulting key
+    order with each key's source (a kept row or an update; later writes win, a key keeps
+    its first-insertion position like the reference's dict)."""
+    plan = _ABPlan()
+    plan.steps = []
+    keys = list(keys0)
     for step in range(n_int):
-        E = Es[step]
-        og = list(probs.keys())
-        ogs = set(og)
-        updates = []
-        for path in og:
-            pm = probs[path]
-            lrows = _branch_rows_ab(path[0], step)
-            rrows = _branch_rows_ab(path[1], step)
-            for l in lrows:
-                for r in rrows:
+        ogs = set(keys)
+        pidx, ms, me, ukeys = [], [], [], []
+        for i, path in enumerate(keys):
+            for l in _branch_rows_ab(path[0], step):
+                for r in _branch_rows_ab(path[1], step):
                     key = (tuple(int(x) for x in l), tuple(int(x) for x in r))
                     if key in ogs and key != path:
                         continue
-                    me = masks[omega_of_key(key)].astype(np.float64)
-                    if step == 0:
-                        res = (pm @ E) * me  # run_markov_chain_AB.py:9-12
-                    else:
-                        ms = masks[omega_of_key(path)].astype(np.float64)
-                        res = (pm * ms) @ E * me
-                    updates.append((key, res))
-            if step > 0:  # steps >= 1 write per path (run_markov_chain_AB.py:262-270)
-                for key, res in updates:
-                    probs[key] = res
-                updates = []
-        for key, res in updates:  # step 0 writes after the loop (only START exists)
-            probs[key] = res
-    return probs
+                    pidx.append(i)
+                    ms.append(masks[omega_of_key(path)])
+                    me.append(masks[omega_of_key(key)])
+                    ukeys.append(key)
+        src = {k: (i, -1) for i, k in enumerate(keys)}
+        for u, k in enumerate(ukeys):
+            src[k] = (-1, u)
+        order = list(src.keys())
+        plan.steps.append((np.asarray(pidx, dtype=np.int64),
+                           np.asarray(ms, dtype=np.float64).reshape(len(pidx), -1),
+                           np.asarray(me, dtype=np.float64).reshape(len(pidx), -1),
+                           np.asarray([src[k][0] for k in order], dtype=np.int64),
+                           np.asarray([src[k][1] for k in order], dtype=np.int64)))
+        keys = order
+    plan.keys = keys
+    return plan
 
 
 _LAST_PLAN: Dict = {}  # n_int -> the plan of the last build (its keys recur every rebuild)
