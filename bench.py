@@ -180,19 +180,21 @@ def pmc_traffic(n, mode, tag_hint=""):
                 # that joins the queue: its per-dispatch average times its launches per call
                 # (the profiled command, scripts/r4/final.sh, makes 3 itr_viterbi calls)
                 def per_call(k, v):
-                    return v["hbm_bytes_raw"] * (max(1, round(v.get("calls", 3) / 3))
-                                                 if "wave_vit_kernel" in k else 1)
+                    return v.get("hbm_bytes_fetch_x2", v["hbm_bytes_raw"]) * (
+                        max(1, round(v.get("calls", 3) / 3)) if "wave_vit_kernel" in k else 1)
                 return round(sum(per_call(k, v) for k, v in parts)), (
                     f"{os.path.basename(f)} (" + " + ".join(k for k, _ in parts) +
-                    "): FETCH_SIZE+WRITE_SIZE per call (all launches of each kernel), raw")
+                    "): 2 x FETCH_SIZE + WRITE_SIZE per call (all launches of each kernel; "
+                    "gfx950 FETCH correction)")
         for name, v in d.items():
             hyb = re.search(r"hybrid_sweep_kernel<\d+, \d+, \d+, (\d+),", name)
             if ((name.startswith("void itr::sweep_kernel<") and
                  name.endswith(f", {mode}>(itr::SweepArgs)")) or
                     (hyb and int(hyb.group(1)) == mode)) and \
                     v.get("n_states", 70) == n and "hbm_bytes_raw" in v:
-                return round(v["hbm_bytes_raw"]), (
-                    f"{os.path.basename(f)} ({name}): FETCH_SIZE+WRITE_SIZE per launch, raw")
+                return round(v.get("hbm_bytes_fetch_x2", v["hbm_bytes_raw"])), (
+                    f"{os.path.basename(f)} ({name}): 2 x FETCH_SIZE + WRITE_SIZE per launch "
+                    "(gfx950 FETCH correction)")
     return None, "no PMC summary under profiles/ for this kernel"
 
 
