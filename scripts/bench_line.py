@@ -2,7 +2,8 @@
 import json
 import sys
 
-d = json.load(open(sys.argv[1]))
+# the last JSON line (RCCL may print its version banner on stdout first)
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 r = d["roofline"]
 print(" ".join(sys.argv[2:]), round(d["value"] / 1e6, 1), "Mcol/s fwd", r.get("forward_ms"),
       "vit", r.get("kernel_ms"), "trace", r.get("traceback_ms"), "fv", r.get("forward_viterbi_ms"),
