@@ -16,6 +16,7 @@
 #include <string>
 #include <chrono>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../../include/itrails_hip.h"
@@ -295,6 +296,10 @@ struct itr_plan {
   // backward sweep concurrently with the forward one; beta rows at d_boff[block]
   int64_t npsplit = 0, beta_rows = 0;
   int64_t* d_boff = nullptr;
+  // hybrid posterior: per-block split column of the longest blocks (0: not split), for the
+  // split set cached in sublo_key (nbeta, first split column fraction)
+  int64_t* d_sublo = nullptr;
+  std::pair<int64_t, double> sublo_key{-1, 0.0};
   double* d_beta = nullptr;
   size_t beta_cap = 0;
   int32_t* d_order = nullptr;
@@ -306,6 +311,7 @@ struct itr_plan {
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
   std::vector<int64_t> sorted_len;  // block lengths, longest first (processing order)
   std::vector<int64_t> h_off;       // block offsets (host copy: the host-block entry points)
+  std::vector<int32_t> h_order;     // processing order (host copy of d_order)
   // forward log-likelihood tasks {block, split, slot} (split blocks: two halves) and the
   // split blocks' scratch
   int64_t ntasks = 0, nsplit = 0;
@@ -630,10 +636,17 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
 // valu / mfma: launch the VALU tasks / the matrix-core groups (both: one launch; one of them:
 // that part only, so the two can run on different CU sets); zero_queues: reset the two work
 // counters on `st` first (a split launch resets them once, before both parts).
+// posterior (matrix-core form): blocks at least this fraction of the longest get their
+// backward sweep beside their forward one (itr_posterior)
+constexpr double kPostBetaFrac = 0.5;
+constexpr double kPostBetaLo = 0.25;  // their split column, as a fraction of their length
+
+// nbeta (posterior, forward-store launch): the first nbeta blocks of the order also get a
+// backward task storing beta rows into v.beta (over [v.sub_lo[block], T)).
 int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const itr::MfmaGeometry& g,
                hipStream_t st, const char* tname, bool valu = true, bool mfma = true,
                int64_t max_grid = -1, bool zero_queues = true, int cus = 0,
-               bool share_cu = false) {
+               bool share_cu = false, int64_t nbeta = 0) {
   if (cus <= 0) cus = cu_count();
   itr::MfmaArgs a{};
   a.n = m->n;
@@ -644,6 +657,7 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
     while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
     v.order = p->d_order;
     v.nblocks = nurg;
+    v.nbeta = mode == itr::MODE_FWD_STORE ? std::min(nbeta, nurg) : 0;
   }
   a.ngroups = ll ? p->ngroups_ll : (p->nblocks - nurg + 3) / 4;
   a.groups = ll ? p->d_groups_ll : p->d_order + nurg;
@@ -662,6 +676,7 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   a.alpha = v.alpha;
   a.astride = g.xr;
   a.post = v.post;
+  a.sink = v.sink;
   a.prio_len = INT32_MAX;
   v.queue = p->d_queue + 3;
   v.prio_len = 0;  // every VALU task of the hybrid is a long block: raised wave priority
@@ -669,13 +684,14 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   // real counter belongs to the concurrent launch of that part)
   if (!valu) {
     v.nblocks = 0;
+    v.nbeta = 0;
     v.queue = p->d_queue + 8;
   }
   if (!mfma) {
     a.ngroups = 0;
     a.queue = p->d_queue + 9;
   }
-  const int64_t work = v.nblocks + (a.ngroups + g.gb - 1) / g.gb;
+  const int64_t work = v.nblocks + v.nbeta + (a.ngroups + g.gb - 1) / g.gb;
   int per_cu = g.per_cu;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_HYB_PER_CU")) per_cu = atoi(getenv("ITR_HYB_PER_CU"));
@@ -865,6 +881,7 @@ int plan_create_impl(const int64_t* off, int64_t nblocks, double split_frac,
   });
   p->sorted_len.resize(nblocks);
   for (int64_t k = 0; k < nblocks; ++k) p->sorted_len[k] = h_off[order[k] + 1] - h_off[order[k]];
+  p->h_order.assign(order.begin(), order.end());
   if (nblocks > 0) {
     const int64_t k = std::min<int64_t>(nblocks - 1, 255);
     const int64_t T = h_off[order[k] + 1] - h_off[order[k]];
@@ -1173,6 +1190,7 @@ int itr_plan_destroy(itr_plan_t p) {
   dev_free(p->d_off);
   dev_free(p->d_tile_off);
   dev_free(p->d_boff);
+  dev_free(p->d_sublo);
   dev_free(p->d_beta);
   dev_free(p->d_order);
   dev_free(p->d_queue);
@@ -1823,9 +1841,61 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
   if (g.cfg >= 0) {
     // forward rows at the hybrid's stride g.xr for every block (reserve() sized for it)
     const itr::MfmaGeometry gb = itr::mfma_geometry(m->n, itr::MODE_BWD);
-    if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, st, "posterior_fwd")) return e;
+    // The longest blocks (at least kPostBetaFrac of the longest) are split at column
+    // lo = kPostBetaLo x T: their backward sweep over [lo, T) (beta rows) runs beside their
+    // forward sweep in the forward launch, the backward launch's VALU task sweeps [0, lo]
+    // from the stored beta_lo, and post_combine forms the posteriors of (lo, T).  A whole
+    // VALU backward + posterior sweep (~0.95 us per column at N = 133) outlasts the
+    // matrix-core bulk of the backward launch.  (Splitting the forward sweep as well — a
+    // forward + posterior sweep over [hi, T) in the backward launch — measured slower: 24.1
+    // against 23.0 ms per (7,7) posterior, profiles/r5ps3_*.)
+    double bfrac = kPostBetaFrac, lofrac = kPostBetaLo;
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_POST_BETA_FRAC")) bfrac = atof(getenv("ITR_POST_BETA_FRAC"));
+    if (getenv("ITR_POST_BETA_LO")) lofrac = atof(getenv("ITR_POST_BETA_LO"));
+#endif
+    int64_t nurg = 0, nbeta = 0, brows = 0;
+    {
+      const double lim = std::max(512.0, g.pfrac * (double)p->sorted_len[0]);  // = run_hybrid
+      while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
+    }
+    const double blim = std::max(512.0, bfrac * (double)p->sorted_len[0]);
+    while (nbeta < std::min(p->npsplit, nurg) && (double)p->sorted_len[nbeta] >= blim)
+      brows += p->sorted_len[nbeta++];
+    if (nbeta > 0 && p->sublo_key != std::make_pair(nbeta, lofrac)) {
+      if (!p->d_sublo)
+        if (int e = dev_alloc(&p->d_sublo, p->nblocks)) return e;
+      std::vector<int64_t> lo(p->nblocks, 0);
+      for (int64_t k = 0; k < nbeta; ++k)  // (blocks >= 512 columns)
+        lo[p->h_order[k]] = std::clamp<int64_t>((int64_t)(lofrac * (double)p->sorted_len[k]), 1,
+                                                p->sorted_len[k] - 2);
+      HIP_TRY(hipMemcpy(p->d_sublo, lo.data(), lo.size() * sizeof(int64_t),
+                        hipMemcpyHostToDevice));
+      p->sublo_key = {nbeta, lofrac};
+    }
+    if (nbeta > 0 && (size_t)brows * g.xr > p->beta_cap) {
+      dev_free(p->d_beta);
+      p->beta_cap = 0;
+      if (int e = dev_alloc(&p->d_beta, (size_t)brows * g.xr)) return e;
+      p->beta_cap = (size_t)brows * g.xr;
+    }
+    if (nbeta > 0) {
+      a.beta = p->d_beta;
+      a.beta_off = p->d_boff;
+      a.sub_lo = p->d_sublo;
+    }
+    if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, st, "posterior_fwd", true, true, -1,
+                           true, 0, false, nbeta))
+      return e;
     a.post = post;
-    return run_hybrid(itr::MODE_BWD, m, p, a, gb, st, "posterior_bwd");
+    a.beta = nullptr;
+    a.beta_in = nbeta > 0 ? p->d_beta : nullptr;
+    if (int e = run_hybrid(itr::MODE_BWD, m, p, a, gb, st, "posterior_bwd")) return e;
+    if (nbeta > 0)
+      HIP_TRY(itr::launch_post_combine(m->n, g.xr, (int)nbeta, p->sorted_len[0], p->d_order,
+                                       p->d_off, p->d_alpha, p->d_beta, p->d_boff, post, st,
+                                       p->d_sublo));
+    return 0;
   }
   const int nl = (int)p->npsplit;
   if (post_split_path(m->n, p)) {

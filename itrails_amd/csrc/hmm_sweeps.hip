@@ -290,15 +290,17 @@ __global__ void __launch_bounds__(256) post_combine_kernel(int n, int xr, const 
                                                            const double* alpha,
                                                            const double* beta,
                                                            const int64_t* beta_off,
-                                                           double* post) {
+                                                           double* post,
+                                                           const int64_t* sub_lo) {
   const int blk = order[blockIdx.y];
   const int64_t c0 = off[blk];
   const int64_t T = off[blk + 1] - c0;
-  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t lo = sub_lo ? sub_lo[blk] : 0;  // first column with a beta row
+  const int64_t t = (sub_lo ? lo + 1 : 0) + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T) return;
   const int l = threadIdx.x & 63;
   const double* a = alpha + (c0 + t) * xr;
-  const double* b = beta + (beta_off[blk] + t) * xr;
+  const double* b = beta + (beta_off[blk] + t - lo) * xr;
   const double q0 = l < n ? a[l] * b[l] : 0.0;
   const double q1 = l + 64 < n ? a[l + 64] * b[l + 64] : 0.0;
   const double q2 = l + 128 < n ? a[l + 128] * b[l + 128] : 0.0;  // (n <= 192)
@@ -312,11 +314,12 @@ __global__ void __launch_bounds__(256) post_combine_kernel(int n, int xr, const 
 
 hipError_t launch_post_combine(int n, int xr, int nlong, int64_t tmax, const int32_t* order,
                                const int64_t* off, const double* alpha, const double* beta,
-                               const int64_t* beta_off, double* post, hipStream_t st) {
+                               const int64_t* beta_off, double* post, hipStream_t st,
+                               const int64_t* sub_lo) {
   if (nlong <= 0 || tmax <= 0) return hipSuccess;
   if (n > 192) return hipErrorInvalidValue;
   hipLaunchKernelGGL(post_combine_kernel, dim3((unsigned)((tmax + 3) / 4), (unsigned)nlong),
-                     dim3(256), 0, st, n, xr, order, off, alpha, beta, beta_off, post);
+                     dim3(256), 0, st, n, xr, order, off, alpha, beta, beta_off, post, sub_lo);
   return hipGetLastError();
 }
 

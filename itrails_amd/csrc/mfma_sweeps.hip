@@ -83,7 +83,10 @@ struct MLds {
   static constexpr size_t rs_off = x_off + (size_t)GB * 2 * 4 * KP * 8;  // RS[GB][2][4][NT]
   static constexpr size_t rm_off = rs_off + (size_t)GB * 2 * NT * 4 * 8; // RM[GB][NT][4]
   static constexpr size_t kf_off = rm_off + (size_t)GB * NT * 4 * 8;     // KF[GB][4]
-  static constexpr size_t bytes = kf_off + (size_t)GB * 4 * 4;
+  // MODE_BWD: alpha * beta rows Q[GB][2][4][16 NT] and their normalisers RN[GB][2][4]
+  static constexpr size_t q_off = kf_off + (size_t)GB * 4 * 4 + 8;
+  static constexpr size_t rn_off = q_off + (size_t)GB * 2 * 4 * 16 * NT * 8;
+  static constexpr size_t bytes = rn_off + (size_t)GB * 2 * 4 * 8;
 };
 
 // y[gb] = x_gb(row ra, sources kk NK ..) @ B for the GB groups of a task.  The A operands
@@ -143,11 +146,13 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
   constexpr int TE = GB == 1 ? 4 : 2;         // columns per prefetch tile
   static_assert(TE >= 2 && 8 % TE == 0, "rescale every 8 steps at tile starts");
   constexpr int TB = 64 * NT;
-  using LD = MLds<NT, NK, GB>;
+  using LD = MLds<NT, NK, GB>;  // (its Q / RN part is used by MODE_BWD only)
   auto X = reinterpret_cast<double (*)[2][4][KP]>(smem + LD::x_off);    // published vectors
   auto RS = reinterpret_cast<double (*)[2][4][NT]>(smem + LD::rs_off);  // row partial sums
   auto RM = reinterpret_cast<double (*)[NT][4]>(smem + LD::rm_off);     // row maxima
   auto KF = reinterpret_cast<int (*)[4]>(smem + LD::kf_off);
+  auto Q = reinterpret_cast<double (*)[2][4][16 * NT]>(smem + LD::q_off);  // BWD: alpha*beta
+  auto RN = reinterpret_cast<double (*)[2][4]>(smem + LD::rn_off);         // BWD: 1 / row sums
 
   const int n = p.n;
   const int tid = threadIdx.x;
@@ -260,6 +265,10 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
         }
         wait_vmem_all();
         lds_barrier();
+        // The forward-store rows run whole tiles and store every step (past a row's end into
+        // the sink): one path through the tile, so the wait for the next tile's loads at its
+        // end does not also wait for the row stores issued after them (vmcnt counts both, in
+        // order, and a skipped store would make the compiler assume the shorter count).
         for (int t0 = 0; t0 < Tmax; t0 += TE) {
           double ecur[GB][TE];
 #pragma unroll
@@ -275,7 +284,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
 #pragma unroll
           for (int sub = 0; sub < TE; ++sub) {
             const int t = t0 + sub;
-            if (t >= 1 && t < Tmax) {
+            if (t >= 1 && (MODE == MODE_FWD_STORE || t < Tmax)) {
               const int buf = (t - 1) & 1;
               double y[GB];
               const double* xs[GB];
@@ -302,7 +311,9 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
                     Kfin[gb] = K[gb];
                   }
                 } else {
-                  if (t < T[gb]) p.alpha[(c0[gb] + t) * p.astride + j] = x[gb];
+                  // past the row's end: the lane's sink slot (a select, not a branch)
+                  double* dst = t < T[gb] ? p.alpha + (c0[gb] + t) * p.astride + j : p.sink + l;
+                  *dst = x[gb];
                 }
                 if (jv) X[gb][buf ^ 1][r][j] = x[gb];
                 if (sub == 0 && (t0 & 7) == 0) {  // every 8th column: maxima for the rescale
@@ -347,27 +358,58 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
         // ---------------- backward + posterior (optimizer.py:191-238)
         //   beta_{T-1} = 1;  beta_{t-1} = (beta_t * e_t) @ a   (vector @ a: the reference's form)
         //   post_t = alpha_t * beta_t / sum_j(alpha_t * beta_t)
-        // Step s handles column t = T - 1 - s of every block of the group.
-        double bt[GB];
+        // Step s handles column t = T - 1 - s of every block of the group.  Only the product
+        // and the vector it publishes sit on the step's critical path, and the normalisation
+        // is taken off the three waves of SIMD 0 (VALU issue there, beside the matrix chain,
+        // is what the step is short of): after barrier s every wave writes its
+        // alpha_t * beta_t values to Q[s & 1]; at step s + 1 one wave (wave 1, on a SIMD with
+        // two waves) sums each row of Q and publishes 1 / sum in RN; at step s + 2 every wave
+        // stores its posterior row of column t (its product kept two steps).  Each array is
+        // read one step after it is written and rewritten one step later: two buffers.  The
+        // loop runs whole tiles, to two steps past the longest row, and every step stores
+        // (lanes with no row into the sink): one path through the tile, so the wait for the
+        // next tile's loads does not also wait for the stores issued after them.
+        double bt[GB], q1[GB], q2[GB];  // alpha * beta of the last two steps
         double anxt[GB][TE];
-        // stored forward row of column T-1-s (unconditional load, see above: an empty row
-        // reads row 0; padded target lanes read stored zeros)
-        auto arow = [&](int gb, int s) -> double {
-          const int tc = max(T[gb] - 1 - s, 0);
-          return p.alpha[(T[gb] > 0 ? c0[gb] + tc : 0) * p.astride + j];
+        // Addresses as a per-row base plus one 32 x 32 -> 64-bit product (v_mad_u64_u32): the
+        // tile's twelve loads and the step's store otherwise cost ~20 VALU instructions each
+        // in 64-bit index arithmetic, and VALU issue — three waves on SIMD 0 — is what this
+        // step is short of beside the matrix chain.  Rows clamp at the block's column 0 (an
+        // empty row reads the arrays' first entries; padded target lanes read stored zeros).
+        const uint16_t* ob[GB];
+        const double* ab[GB];
+        double* pb[GB];
+#pragma unroll
+        for (int gb = 0; gb < GB; ++gb) {
+          const int64_t cb = T[gb] > 0 ? c0[gb] : 0;
+          ob[gb] = p.obs + cb;
+          ab[gb] = p.alpha + cb * p.astride + j;
+          pb[gb] = p.post + cb * n + j;
+        }
+        const double* eb = p.emit + jc;
+        const uint32_t ast = (uint32_t)p.astride, un = (uint32_t)n;
+        auto bsym = [&](int gb, int s) -> int {  // symbol of column T-1-s
+          return (int)ob[gb][max(T[gb] - 1 - s, 0)];
+        };
+        auto bemis = [&](int sy) -> double { return eb[(uint64_t)(uint32_t)min(sy, 624) * un]; };
+        auto arow = [&](int gb, int s) -> double {  // stored forward row of column T-1-s
+          return ab[gb][(uint64_t)(uint32_t)max(T[gb] - 1 - s, 0) * ast];
         };
 #pragma unroll
         for (int gb = 0; gb < GB; ++gb) {
           bt[gb] = (T[gb] > 0 && jv) ? 1.0 : 0.0;
+          q1[gb] = q2[gb] = 0.0;
 #pragma unroll
           for (int u = 0; u < TE; ++u) {
-            enxt[gb][u] = emis(sym(gb, T[gb] - 1 - u));
+            enxt[gb][u] = bemis(bsym(gb, u));
             anxt[gb][u] = arow(gb, u);
-            snxt[gb][u] = sym(gb, T[gb] - 1 - (TE + u));
+            snxt[gb][u] = bsym(gb, TE + u);
           }
         }
         wait_vmem_all();
-        for (int s0 = 0; s0 < Tmax; s0 += TE) {
+        const bool norm_wave = w == 1;
+        const int nl = l & 15;  // the norm wave: lane nl of row r sums Q[..][r][nl NT ..]
+        for (int s0 = 0; s0 < Tmax + 2; s0 += TE) {
           double ecur[GB][TE], acur[GB][TE];
 #pragma unroll
           for (int gb = 0; gb < GB; ++gb) {
@@ -378,50 +420,71 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
             }
 #pragma unroll
             for (int u = 0; u < TE; ++u) {
-              enxt[gb][u] = emis(snxt[gb][u]);
+              enxt[gb][u] = bemis(snxt[gb][u]);
               anxt[gb][u] = arow(gb, s0 + TE + u);
-              snxt[gb][u] = sym(gb, T[gb] - 1 - (s0 + 2 * TE + u));
+              snxt[gb][u] = bsym(gb, s0 + 2 * TE + u);
             }
           }
 #pragma unroll
           for (int sub = 0; sub < TE; ++sub) {
             const int s = s0 + sub;
-            if (s < Tmax) {
-              const int buf = s & 1;
-              double qv[GB];
+            const int buf = sub & 1;  // s0 is a multiple of TE (even)
+            const bool rescale = sub == 0 && (s0 & 7) == 0;
 #pragma unroll
-              for (int gb = 0; gb < GB; ++gb) {
-                qv[gb] = acur[gb][sub] * bt[gb];  // padded states: 0 * 0
-                const double v = bt[gb] * ecur[gb][sub];
-                const double ps = row16_sum(qv[gb]);
-                if (row_leader) RS[gb][buf][r][w] = ps;
-                if (sub == 0 && (s0 & 7) == 0) {
-                  const double m = row16_max(v);
-                  if (row_leader) RM[gb][w][r] = m;
-                }
-                if (jv) X[gb][buf][r][j] = v;
+            for (int gb = 0; gb < GB; ++gb) {
+              const double v = bt[gb] * ecur[gb][sub];
+              if (rescale) {
+                const double m = row16_max(v);
+                if (row_leader) RM[gb][w][r] = m;
               }
-              lds_barrier();
-              // the matrix products first; the columns' normalisation (a log-depth tree over
-              // the NT wave partials) and the rescale maximum while they run
-              double y[GB];
-              const double* xs[GB];
+              if (jv) X[gb][buf][r][j] = v;
+            }
+            lds_barrier();
+            // the normalisers of step s - 2 (published at step s - 1) and, on the norm wave,
+            // the products of step s - 1
+            double rn[GB], qs[GB][NT];
 #pragma unroll
-              for (int gb = 0; gb < GB; ++gb) xs[gb] = &X[gb][buf][ra][kk * NK];
-              mfma_chain<NK, GB>(xs, B, y);
+            for (int gb = 0; gb < GB; ++gb) {
+              rn[gb] = RN[gb][buf][r];
+              if (norm_wave) {
 #pragma unroll
-              for (int gb = 0; gb < GB; ++gb) {
-                const double rS = recip_nr(tree_sum<NT>(&RS[gb][buf][r][0]));
-                if (s < T[gb] && jv) p.post[(c0[gb] + (T[gb] - 1 - s)) * n + j] = qv[gb] * rS;
-                double sc = 1.0;
-                if (sub == 0 && (s0 & 7) == 0) {
-                  double M = RM[gb][0][r];
-#pragma unroll
-                  for (int v = 1; v < NT; ++v) M = fmax(M, RM[gb][v][r]);
-                  if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
-                }
-                bt[gb] = y[gb] * sc;
+                for (int v = 0; v < NT; ++v) qs[gb][v] = Q[gb][buf ^ 1][r][nl * NT + v];
               }
+            }
+#pragma unroll
+            for (int gb = 0; gb < GB; ++gb) {
+              const double qv = acur[gb][sub] * bt[gb];  // padded states: 0 * 0
+              Q[gb][buf][r][j] = qv;
+              if (norm_wave) {
+                double S = qs[gb][0];
+#pragma unroll
+                for (int v = 1; v < NT; ++v) S += qs[gb][v];
+                S = row16_sum(S);
+                if (row_leader) RN[gb][buf ^ 1][r] = recip_nr(S);
+              }
+              const int sp = s - 2;  // the column of step s - 2
+              double* dst = (sp >= 0 && sp < T[gb] && jv)
+                                ? pb[gb] + (uint64_t)(uint32_t)(T[gb] - 1 - sp) * un
+                                : p.sink + l;
+              *dst = q2[gb] * rn[gb];
+              q2[gb] = q1[gb];
+              q1[gb] = qv;
+            }
+            double y[GB];
+            const double* xs[GB];
+#pragma unroll
+            for (int gb = 0; gb < GB; ++gb) xs[gb] = &X[gb][buf][ra][kk * NK];
+            mfma_chain<NK, GB>(xs, B, y);
+#pragma unroll
+            for (int gb = 0; gb < GB; ++gb) {
+              double sc = 1.0;
+              if (rescale) {  // (the maxima read here: before the chain their registers spill)
+                double M = RM[gb][0][r];
+#pragma unroll
+                for (int v = 1; v < NT; ++v) M = fmax(M, RM[gb][v][r]);
+                if (M > 0.0 && M < INFINITY) sc = ldexp(1.0, -ilogb(M));
+              }
+              bt[gb] = y[gb] * sc;
             }
           }
         }
@@ -441,13 +504,28 @@ __global__ void __launch_bounds__(64 * NT, (MOcc<NT, NK, GB, MODE>::value))
     hybrid_sweep_kernel(MfmaArgs p, SweepArgs v) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int qslot[2];
+  // VALU tasks.  The posterior splits its first v.nbeta (longest) blocks at column lo
+  // (v.sub_lo): the forward-store launch runs, beside each one's forward sweep, its backward
+  // sweep over [lo, T) storing beta rows (task 2k: block k backward, 2k + 1: forward); the
+  // backward launch's VALU task then sweeps only [0, lo] from the stored beta_lo, and
+  // post_combine forms the columns (lo, T).  The longest block then costs one sweep of its
+  // length in the forward launch and lo columns in the backward one, instead of two whole
+  // sweeps one after the other.
+  const int64_t nvalu = v.nblocks + (MODE == MODE_FWD_STORE ? v.nbeta : 0);
   for (;;) {
     if (threadIdx.x == 0) qslot[0] = atomicAdd(v.queue, 1);
     lds_barrier();
     const int bi = uni(qslot[0]);
     lds_barrier();
-    if (bi >= v.nblocks) break;
-    sweep_task<8, NT, VRJ, VIQ, MODE>(v, smem, bi);
+    if (bi >= nvalu) break;
+    if (MODE == MODE_FWD_STORE && bi < 2 * v.nbeta) {
+      if (bi & 1)
+        sweep_task<8, NT, VRJ, VIQ, MODE_FWD_STORE>(v, smem, bi >> 1);
+      else
+        sweep_task<8, NT, VRJ, VIQ, MODE_BWD>(v, smem, bi >> 1);
+    } else {
+      sweep_task<8, NT, VRJ, VIQ, MODE>(v, smem, MODE == MODE_FWD_STORE ? bi - (int)v.nbeta : bi);
+    }
   }
   for (;;) {
     if (threadIdx.x == 0) qslot[1] = atomicAdd(p.queue, GB);
@@ -483,7 +561,9 @@ constexpr int kMCfgsAuto = 7;  // entries picked by state count
 template <int NT, int NK, int GB, int MODE, int VIQ>
 size_t lds_h() {
   using V = ValuSweep<8, NT, 2, VIQ, MODE>;
-  return std::max(MLds<NT, NK, GB>::bytes, V::lds_bytes);
+  // forward-store launches also run backward (beta) tasks
+  using VB = ValuSweep<8, NT, 2, VIQ, MODE == MODE_FWD_STORE ? MODE_BWD : MODE>;
+  return std::max(MLds<NT, NK, GB>::bytes, std::max(V::lds_bytes, VB::lds_bytes));
 }
 template <int NT, int NK, int GB, int MODE, int VIQ>
 hipError_t launch_h(const MfmaArgs& a, const SweepArgs& v, int grid, size_t lds_min,

@@ -38,6 +38,14 @@ struct SweepArgs {
   double* beta;                 // MODE_BWD, optional: store the backward rows beta_t here
                                 //   (row beta_off[block] + t, stride XR) instead of posteriors
   const int64_t* beta_off;      //   [nblocks] first beta row of every split block
+  int64_t nbeta;                // hybrid MODE_FWD_STORE: the first nbeta blocks of `order`
+                                //   also get a backward task storing beta rows (see
+                                //   mfma_sweeps.hip); 0 elsewhere
+  const int64_t* sub_lo;        // MODE_BWD, optional, [nblocks]: lo > 0 splits the block at
+                                //   column lo: a beta task (beta set) sweeps columns [lo, T)
+                                //   only, storing beta_lo .. beta_{T-1}; a posterior task
+                                //   sweeps columns [0, lo] only, from beta_lo (beta_in)
+  const double* beta_in;        //   the stored beta rows the posterior tasks start from
   const int32_t* tasks;         // MODE_FWD_LL: [nblocks x 3] {block, split, slot}, see capi.cpp
   double* svec;                 // MODE_FWD_LL: [nsplit x 2 x XR] vectors of split blocks
   int* sK;                      // MODE_FWD_LL: [nsplit x 2] their power-of-two exponents
@@ -64,9 +72,12 @@ int sweep_row_stride(int n, int mode);
 // post_combine forms alpha_t beta_t / sum_j alpha_t beta_t for those blocks' columns.
 hipError_t launch_post_split(const SweepGeometry& g, int grid, const SweepArgs& f,
                              const SweepArgs& b, int nlong, hipStream_t st);
+// sub_lo (optional): the blocks' beta rows start at column sub_lo[block] (row beta_off +
+// t - lo) and only columns (lo, T) are formed (the posterior task did [0, lo])
 hipError_t launch_post_combine(int n, int xr, int nlong, int64_t tmax, const int32_t* order,
                                const int64_t* off, const double* alpha, const double* beta,
-                               const int64_t* beta_off, double* post, hipStream_t st);
+                               const int64_t* beta_off, double* post, hipStream_t st,
+                               const int64_t* sub_lo = nullptr);
 hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepArgs& a,
                         hipStream_t st);
 
@@ -89,6 +100,8 @@ struct MfmaArgs {
   double* alpha;                // forward rows, row stride astride (FWD_STORE out, BWD in)
   int64_t astride;
   double* post;                 // [total x n]                (MODE_BWD)
+  double* sink;                 // [64] store target of lanes with no row to write (FWD_STORE,
+                                //   BWD): every step stores unconditionally, no branch
   double* svec;                 // MODE_FWD_LL: split halves' vectors [slots x 2 x astride]
   int* sK;                      // MODE_FWD_LL: their power-of-two exponents [slots x 2]
   int prio_len;                 // groups at least this long run at raised wave priority

@@ -384,8 +384,19 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
     const int blk = uni(td ? td[0] : p.order[bi]);
     const int split = td ? uni(td[1]) : 0;
     const int slot = td ? uni(td[2]) : 0;
-    const int64_t c0 = p.off[blk];
-    const int Tb = uni((int)(p.off[blk + 1] - c0));
+    int64_t c0 = p.off[blk];
+    int Tb = uni((int)(p.off[blk + 1] - c0));
+    // a block split at column lo (hybrid posterior, p.sub_lo): the beta task takes columns
+    // [lo, T), the posterior task columns [0, lo] — each as a block of its own
+    const int lo = (MODE == MODE_BWD && p.sub_lo) ? uni((int)p.sub_lo[blk]) : 0;
+    if (lo > 0) {
+      if (p.beta) {
+        c0 += lo;
+        Tb -= lo;
+      } else {
+        Tb = lo + 1;
+      }
+    }
     // steps + 1 of this task: the backward half runs Tb - m steps
     const int T = split > 0 ? split : (split < 0 ? Tb + split + 1 : Tb);
     // NOTE: no `continue` in this loop.  With a barrier in the body, hipcc (ROCm 7.2)
@@ -591,7 +602,14 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
         // unrolled tile keeps the periodic work branch-free like the forward sweep.
         double bt[RJN];
 #pragma unroll
-        for (int r = 0; r < RJN; ++r) bt[r] = jv[r] ? 1.0 : 0.0;
+        for (int r = 0; r < RJN; ++r) {
+          // a split block's posterior task starts from the stored beta_lo (rescaled like any
+          // beta row: the posterior is invariant to a power-of-two factor per column)
+          if (lo > 0 && !p.beta)
+            bt[r] = jv[r] ? p.beta_in[p.beta_off[blk] * XR + jr[r]] : 0.0;
+          else
+            bt[r] = jv[r] ? 1.0 : 0.0;
+        }
         // posterior rows through a buffer resource on the block's rows: lane offset = its
         // state (padded states: out of range, nothing stored), row offset in a scalar register
         // (blocks whose rows span 4 GiB or more store through 64-bit addresses instead)
