@@ -307,7 +307,8 @@ struct itr_plan {
                            // [3, 4] hybrid sweeps, [5, 6] Viterbi hybrid, [7] per-wave Viterbi,
                            // [8, 9] the idle loop of a split hybrid launch, [10] per-wave forward,
                            // [12] mixed launch, [13] the long blocks' traceback
-  double* d_sink = nullptr;  // write target of padded states (64 doubles)
+  double* d_sink = nullptr;  // write target of padded states (64 doubles per workgroup,
+                             // itr::kSinkWgs of them)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
   std::vector<int64_t> sorted_len;  // block lengths, longest first (processing order)
   std::vector<int64_t> h_off;       // block offsets (host copy: the host-block entry points)
@@ -1128,7 +1129,7 @@ int plan_create_impl(const int64_t* off, int64_t nblocks, double split_frac,
   if (!e) e = dev_alloc(&p->d_queue, 16);
   if (!e && hipMemset(p->d_queue, 0, 16 * sizeof(int)) != hipSuccess)
     e = fail(ITR_EHIP, "plan workspace init failed");
-  if (!e) e = dev_alloc(&p->d_sink, 64);
+  if (!e) e = dev_alloc(&p->d_sink, 64 * (size_t)itr::kSinkWgs);
   if (!e) e = dev_alloc(&p->d_last, nblocks);
   auto up = [&](void* d, const void* h, size_t bytes) {
     if (e || bytes == 0) return;

@@ -76,7 +76,7 @@ __device__ __forceinline__ int group_member(const MfmaArgs& p, int gi, int rr) {
 }
 
 // LDS of one matrix-core task (carved from the kernel's dynamic LDS)
-template <int NT, int NK, int GB>
+template <int NT, int NK, int GB, bool BWD = false>
 struct MLds {
   static constexpr int KP = 4 * NK;
   static constexpr size_t x_off = 0;                                   // X[GB][2][4][KP]
@@ -86,7 +86,7 @@ struct MLds {
   // MODE_BWD: alpha * beta rows Q[GB][2][4][16 NT] and their normalisers RN[GB][2][4]
   static constexpr size_t q_off = kf_off + (size_t)GB * 4 * 4 + 8;
   static constexpr size_t rn_off = q_off + (size_t)GB * 2 * 4 * 16 * NT * 8;
-  static constexpr size_t bytes = rn_off + (size_t)GB * 2 * 4 * 8;
+  static constexpr size_t bytes = BWD ? rn_off + (size_t)GB * 2 * 4 * 8 : q_off;
 };
 
 // y[gb] = x_gb(row ra, sources kk NK ..) @ B for the GB groups of a task.  The A operands
@@ -146,7 +146,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
   constexpr int TE = GB == 1 ? 4 : 2;         // columns per prefetch tile
   static_assert(TE >= 2 && 8 % TE == 0, "rescale every 8 steps at tile starts");
   constexpr int TB = 64 * NT;
-  using LD = MLds<NT, NK, GB>;  // (its Q / RN part is used by MODE_BWD only)
+  using LD = MLds<NT, NK, GB, MODE == MODE_BWD>;
   auto X = reinterpret_cast<double (*)[2][4][KP]>(smem + LD::x_off);    // published vectors
   auto RS = reinterpret_cast<double (*)[2][4][NT]>(smem + LD::rs_off);  // row partial sums
   auto RM = reinterpret_cast<double (*)[NT][4]>(smem + LD::rm_off);     // row maxima
@@ -163,6 +163,9 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
   const int ra = l & 3, kk = l >> 4;               // A operand: block row, k-lane
   const bool jv = j < n;
   const bool row_leader = (l & 15) == 0;
+  // this lane's sink slot: one 64-double line set per workgroup (kSinkWgs of them), so the
+  // discarded stores of different CUs never share a cache line
+  double* const sink = p.sink + (int64_t)(blockIdx.x % kSinkWgs) * 64 + l;
 
   // Rows of the group(s).  MODE_FWD_LL: p.groups holds task ids of p.tasks {block, split,
   // slot} — whole blocks (split 0), first halves (split m > 0: columns [0, m)) or second
@@ -312,7 +315,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
                   }
                 } else {
                   // past the row's end: the lane's sink slot (a select, not a branch)
-                  double* dst = t < T[gb] ? p.alpha + (c0[gb] + t) * p.astride + j : p.sink + l;
+                  double* dst = t < T[gb] ? p.alpha + (c0[gb] + t) * p.astride + j : sink;
                   *dst = x[gb];
                 }
                 if (jv) X[gb][buf ^ 1][r][j] = x[gb];
@@ -465,7 +468,7 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
               const int sp = s - 2;  // the column of step s - 2
               double* dst = (sp >= 0 && sp < T[gb] && jv)
                                 ? pb[gb] + (uint64_t)(uint32_t)(T[gb] - 1 - sp) * un
-                                : p.sink + l;
+                                : sink;
               *dst = q2[gb] * rn[gb];
               q2[gb] = q1[gb];
               q1[gb] = qv;
@@ -522,7 +525,7 @@ __global__ void __launch_bounds__(64 * NT, (MOcc<NT, NK, GB, MODE>::value))
       if (bi & 1)
         sweep_task<8, NT, VRJ, VIQ, MODE_FWD_STORE>(v, smem, bi >> 1);
       else
-        sweep_task<8, NT, VRJ, VIQ, MODE_BWD>(v, smem, bi >> 1);
+        sweep_task<8, NT, VRJ, VIQ, MODE_BETA>(v, smem, bi >> 1);
     } else {
       sweep_task<8, NT, VRJ, VIQ, MODE>(v, smem, MODE == MODE_FWD_STORE ? bi - (int)v.nbeta : bi);
     }
@@ -562,8 +565,8 @@ template <int NT, int NK, int GB, int MODE, int VIQ>
 size_t lds_h() {
   using V = ValuSweep<8, NT, 2, VIQ, MODE>;
   // forward-store launches also run backward (beta) tasks
-  using VB = ValuSweep<8, NT, 2, VIQ, MODE == MODE_FWD_STORE ? MODE_BWD : MODE>;
-  return std::max(MLds<NT, NK, GB>::bytes, std::max(V::lds_bytes, VB::lds_bytes));
+  using VB = ValuSweep<8, NT, 2, VIQ, MODE == MODE_FWD_STORE ? MODE_BETA : MODE>;
+  return std::max(MLds<NT, NK, GB, MODE == MODE_BWD>::bytes, std::max(V::lds_bytes, VB::lds_bytes));
 }
 template <int NT, int NK, int GB, int MODE, int VIQ>
 hipError_t launch_h(const MfmaArgs& a, const SweepArgs& v, int grid, size_t lds_min,

@@ -6,7 +6,15 @@
 
 namespace itr {
 
-enum SweepMode { MODE_FWD_LL = 0, MODE_FWD_STORE = 1, MODE_BWD = 2, MODE_VIT = 3 };
+enum SweepMode {
+  MODE_FWD_LL = 0,
+  MODE_FWD_STORE = 1,
+  MODE_BWD = 2,
+  MODE_VIT = 3,
+  // the backward sweep storing beta rows only (the hybrid posterior's split blocks, inside
+  // the forward-store launch): MODE_BWD's arithmetic without its posterior code
+  MODE_BETA = 4
+};
 
 // Viterbi columns per tile: one omega checkpoint row and one 16-bit stay-flag word per
 // state per tile of every block (tiles start at each block's first column)
@@ -82,6 +90,7 @@ hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepA
                         hipStream_t st);
 
 // Matrix-core sweeps (mfma_sweeps.hip): groups of four blocks advanced in lock-step
+constexpr int kSinkWgs = 1024;  // workgroups with a sink line set of their own (MfmaArgs.sink)
 struct MfmaArgs {
   int n;                        // hidden states
   int64_t ngroups;
@@ -100,8 +109,8 @@ struct MfmaArgs {
   double* alpha;                // forward rows, row stride astride (FWD_STORE out, BWD in)
   int64_t astride;
   double* post;                 // [total x n]                (MODE_BWD)
-  double* sink;                 // [64] store target of lanes with no row to write (FWD_STORE,
-                                //   BWD): every step stores unconditionally, no branch
+  double* sink;                 // [kSinkWgs x 64] store target of lanes with no row to write
+                                //   (FWD_STORE, BWD): every step stores unconditionally
   double* svec;                 // MODE_FWD_LL: split halves' vectors [slots x 2 x astride]
   int* sK;                      // MODE_FWD_LL: their power-of-two exponents [slots x 2]
   int prio_len;                 // groups at least this long run at raised wave priority

@@ -388,9 +388,10 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
     int Tb = uni((int)(p.off[blk + 1] - c0));
     // a block split at column lo (hybrid posterior, p.sub_lo): the beta task takes columns
     // [lo, T), the posterior task columns [0, lo] — each as a block of its own
-    const int lo = (MODE == MODE_BWD && p.sub_lo) ? uni((int)p.sub_lo[blk]) : 0;
+    const int lo = ((MODE == MODE_BWD || MODE == MODE_BETA) && p.sub_lo)
+                       ? uni((int)p.sub_lo[blk]) : 0;
     if (lo > 0) {
-      if (p.beta) {
+      if (MODE == MODE_BETA || p.beta) {
         c0 += lo;
         Tb -= lo;
       } else {
@@ -421,7 +422,8 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
           }
         }
       }
-      ObsTiles ot{OBS, p.obs + c0, Tb, (MODE == MODE_BWD || split < 0) ? -1 : +1, TB, 0};
+      ObsTiles ot{OBS, p.obs + c0, Tb,
+                  (MODE == MODE_BWD || MODE == MODE_BETA || split < 0) ? -1 : +1, TB, 0};
       ot.start(tid);
       lds_barrier();
       auto sym_row = [&](int s) -> int64_t {
@@ -593,7 +595,7 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
             p.loglik[blk] = log(tot) + (double)K * LN2;
           }
         }
-      } else if constexpr (MODE == MODE_BWD) {
+      } else if constexpr (MODE == MODE_BWD || MODE == MODE_BETA) {
         // ------------- backward + posterior (optimizer.py:191-238)
         //   beta_{T-1} = 1;  beta_{t-1} = (beta_t * e_t) @ a  (vector @ a: the reference's form)
         //   post_t = alpha_t * beta_t / sum_j(alpha_t * beta_t)
@@ -605,7 +607,7 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
         for (int r = 0; r < RJN; ++r) {
           // a split block's posterior task starts from the stored beta_lo (rescaled like any
           // beta row: the posterior is invariant to a power-of-two factor per column)
-          if (lo > 0 && !p.beta)
+          if (MODE == MODE_BWD && lo > 0 && !p.beta)
             bt[r] = jv[r] ? p.beta_in[p.beta_off[blk] * XR + jr[r]] : 0.0;
           else
             bt[r] = jv[r] ? 1.0 : 0.0;
@@ -687,9 +689,10 @@ __device__ __forceinline__ void sweep_task(const SweepArgs& p, unsigned char* sm
 #pragma unroll
                 for (int r = 0; r < RJN; ++r) acc[k % NCH][r] = fma(xi, m[k][r], acc[k % NCH][r]);
               }
-              if (p.beta) {
-                // concurrent split (launch_post_split): this block's forward rows are being
-                // written by another workgroup, so store beta_t for post_combine instead
+              if (MODE == MODE_BETA || p.beta) {
+                // concurrent split (launch_post_split, the hybrid's beta tasks): this block's
+                // forward rows are being written by another workgroup, so store beta_t for
+                // post_combine instead
                 const int64_t brow = (p.beta_off[blk] + t) * XR;
 #pragma unroll
                 for (int r = 0; r < RJN; ++r) p.beta[brow + jr[r]] = bt[r];
