@@ -658,7 +658,7 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
     while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
     v.order = p->d_order;
     v.nblocks = nurg;
-    v.nbeta = mode == itr::MODE_FWD_STORE ? std::min(nbeta, nurg) : 0;
+    v.nbeta = mode == itr::MODE_FWD_STORE ? nbeta : 0;
   }
   a.ngroups = ll ? p->ngroups_ll : (p->nblocks - nurg + 3) / 4;
   a.groups = ll ? p->d_groups_ll : p->d_order + nurg;
@@ -1855,9 +1855,11 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
     if (getenv("ITR_POST_BETA_FRAC")) bfrac = atof(getenv("ITR_POST_BETA_FRAC"));
     if (getenv("ITR_POST_BETA_LO")) lofrac = atof(getenv("ITR_POST_BETA_LO"));
 #endif
+    // (split blocks are VALU tasks of the backward launch: a prefix of its VALU set, whose
+    // limit mirrors run_hybrid's; their forward sweep is a VALU task or a matrix-core group)
     int64_t nurg = 0, nbeta = 0, brows = 0;
     {
-      const double lim = std::max(512.0, g.pfrac * (double)p->sorted_len[0]);  // = run_hybrid
+      const double lim = std::max(512.0, gb.pfrac * (double)p->sorted_len[0]);
       while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
     }
     const double blim = std::max(512.0, bfrac * (double)p->sorted_len[0]);

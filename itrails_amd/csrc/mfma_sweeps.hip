@@ -514,20 +514,26 @@ __global__ void __launch_bounds__(64 * NT, (MOcc<NT, NK, GB, MODE>::value))
   // post_combine forms the columns (lo, T).  The longest block then costs one sweep of its
   // length in the forward launch and lo columns in the backward one, instead of two whole
   // sweeps one after the other.
-  const int64_t nvalu = v.nblocks + (MODE == MODE_FWD_STORE ? v.nbeta : 0);
+  // (the forward tasks are the first v.nblocks blocks of the order, the beta tasks the first
+  // v.nbeta: the two sets interleaved longest first, then the longer set's rest)
+  const int nb = MODE == MODE_FWD_STORE ? (int)v.nbeta : 0;
+  const int np = min((int)v.nblocks, nb);
+  const int64_t nvalu = v.nblocks + nb;
   for (;;) {
     if (threadIdx.x == 0) qslot[0] = atomicAdd(v.queue, 1);
     lds_barrier();
     const int bi = uni(qslot[0]);
     lds_barrier();
     if (bi >= nvalu) break;
-    if (MODE == MODE_FWD_STORE && bi < 2 * v.nbeta) {
+    if (MODE == MODE_FWD_STORE && bi < 2 * np) {
       if (bi & 1)
         sweep_task<8, NT, VRJ, VIQ, MODE_FWD_STORE>(v, smem, bi >> 1);
       else
         sweep_task<8, NT, VRJ, VIQ, MODE_BETA>(v, smem, bi >> 1);
+    } else if (MODE == MODE_FWD_STORE && nb > np) {
+      sweep_task<8, NT, VRJ, VIQ, MODE_BETA>(v, smem, bi - np);
     } else {
-      sweep_task<8, NT, VRJ, VIQ, MODE>(v, smem, MODE == MODE_FWD_STORE ? bi - (int)v.nbeta : bi);
+      sweep_task<8, NT, VRJ, VIQ, MODE>(v, smem, bi - np);
     }
   }
   for (;;) {
@@ -548,17 +554,19 @@ struct MCfg {
   double pfrac;  // posterior: blocks longer than pfrac x the longest run as VALU tasks
   bool post;     // the hybrid posterior beats the VALU-only one at this size
 };
-// pfrac measured on the (7,7) model, 10 Mbp (scripts/gpu_post133.sh: 0.2 / 0.35 / 0.5 / 0.7
-// -> 203 / 264 / 281 / 259 M columns/s) and the (5,5) model (scripts/gpu_r2b.sh)
+// pfrac measured on the (7,7) model, 10 Mbp (round 2: 0.2 / 0.35 / 0.5 / 0.7 -> 203 / 264 /
+// 281 / 259 M columns/s; round 5, with the long blocks' backward split (itr_posterior):
+// 0.45 / 0.5 / 0.55 / 0.6 / 0.65 -> 23.9 / 22.8 / 22.4 / 23.1 / 25.1 ms, per-launch
+// fractions no better, profiles/r5ab_posterior_variants.txt) and the (5,5) model
 // (the (5,5) model, N = 70: hybrid posterior 465 M columns/s against 496 for the VALU-only
 // three-wave sweeps, so the posterior stays VALU-only up to N = 96)
 constexpr MCfg kMCfgs[] = {
     {33, 48, 3, 12, 1, 6, 0.35, false},   {49, 64, 4, 16, 1, 8, 0.35, false},
     {65, 72, 5, 18, 1, 9, 0.35, false},   {73, 80, 5, 20, 1, 10, 0.35, false},
-    {81, 96, 6, 24, 1, 12, 0.35, false},  {129, 136, 9, 34, 1, 17, 0.5, true},
-    {137, 144, 9, 36, 1, 18, 0.5, true},
+    {81, 96, 6, 24, 1, 12, 0.35, false},  {129, 136, 9, 34, 1, 17, 0.55, true},
+    {137, 144, 9, 36, 1, 18, 0.55, true},
     // two groups per workgroup (experiment configuration, ITR_MCFG)
-    {129, 136, 9, 34, 2, 17, 0.5, true}};
+    {129, 136, 9, 34, 2, 17, 0.55, true}};
 constexpr int kMCfgsAuto = 7;  // entries picked by state count
 
 template <int NT, int NK, int GB, int MODE, int VIQ>
@@ -648,6 +656,10 @@ MfmaGeometry mfma_geometry(int n, int mode) {
   g.pfrac = kMCfgs[g.cfg].pfrac;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_POST_URGENT_FRAC")) g.pfrac = atof(getenv("ITR_POST_URGENT_FRAC"));
+  if (mode == MODE_FWD_STORE && getenv("ITR_POST_URGENT_FRAC_F"))
+    g.pfrac = atof(getenv("ITR_POST_URGENT_FRAC_F"));
+  if (mode == MODE_BWD && getenv("ITR_POST_URGENT_FRAC_B"))
+    g.pfrac = atof(getenv("ITR_POST_URGENT_FRAC_B"));
 #endif
   int occ = 1;
   (void)dispatch_mode_m(mode, g.cfg, false, nullptr, nullptr, 0, 0, nullptr, &occ);
