@@ -640,7 +640,7 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
 // posterior (matrix-core form): blocks at least this fraction of the longest get their
 // backward sweep beside their forward one (itr_posterior)
 constexpr double kPostBetaFrac = 0.5;
-constexpr double kPostBetaLo = 0.25;  // their split column, as a fraction of their length
+constexpr double kPostBetaLo = 0.4;  // their split column, as a fraction of their length
 
 // nbeta (posterior, forward-store launch): the first nbeta blocks of the order also get a
 // backward task storing beta rows into v.beta (over [v.sub_lo[block], T)).
@@ -1894,6 +1894,8 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
     a.beta = nullptr;
     a.beta_in = nbeta > 0 ? p->d_beta : nullptr;
     if (int e = run_hybrid(itr::MODE_BWD, m, p, a, gb, st, "posterior_bwd")) return e;
+    // (post_combine beside the backward launch, on a side stream, delayed that launch's
+    // workgroups by as much as it saved: 22.25 against 22.18 ms, profiles/r5ptl3_*)
     if (nbeta > 0)
       HIP_TRY(itr::launch_post_combine(m->n, g.xr, (int)nbeta, p->sorted_len[0], p->d_order,
                                        p->d_off, p->d_alpha, p->d_beta, p->d_boff, post, st,
