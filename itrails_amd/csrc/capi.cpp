@@ -544,9 +544,10 @@ void plan_partition(itr_plan_t p, const std::vector<int64_t>& ulen, int cus) {
 // (latency-bound: 10 Mbp in 100 blocks of 100 kbp, 96.9 -> 60 ms); with thousands of blocks
 // the sweeps are throughput-bound and the extra beta rows cost more than the shorter tail
 // (chr10: 20.7 vs 23.4 ms).  reserve() sizes the beta rows by the same test.
+// (the VALU-only concurrent split takes few-block workloads at N <= 128 even where the
+// matrix-core posterior exists: 100 blocks of 100 kbp at N = 70, 51.3 against 61.4 ms)
 bool post_split_path(int n, itr_plan_t p) {
-  return p->npsplit > 0 && n <= 128 && p->nblocks <= 2 * (int64_t)cu_count() &&
-         itr::mfma_geometry(n, itr::MODE_FWD_STORE).cfg < 0;
+  return p->npsplit > 0 && n <= 128 && p->nblocks <= 2 * (int64_t)cu_count();
 }
 
 int reserve(itr_plan_t p, int n, bool vit, bool post) {
@@ -1839,7 +1840,7 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
   a.init = m->PIE;
   a.alpha = p->d_alpha;
   const itr::MfmaGeometry g = itr::mfma_geometry(m->n, itr::MODE_FWD_STORE);
-  if (g.cfg >= 0) {
+  if (g.cfg >= 0 && !post_split_path(m->n, p)) {
     // forward rows at the hybrid's stride g.xr for every block (reserve() sized for it)
     const itr::MfmaGeometry gb = itr::mfma_geometry(m->n, itr::MODE_BWD);
     // The longest blocks (at least kPostBetaFrac of the longest) are split at column

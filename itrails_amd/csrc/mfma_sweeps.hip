@@ -559,10 +559,12 @@ struct MCfg {
 // 0.45 / 0.5 / 0.55 / 0.6 / 0.65 -> 23.9 / 22.8 / 22.4 / 23.1 / 25.1 ms, per-launch
 // fractions no better, profiles/r5ab_posterior_variants.txt) and the (5,5) model
 // (the (5,5) model, N = 70: hybrid posterior 465 M columns/s against 496 for the VALU-only
-// three-wave sweeps, so the posterior stays VALU-only up to N = 96)
+// three-wave sweeps in round 2; with round 5's backward step and split, 668-685 against
+// 521-523 M (profiles/r5ab55*): the hybrid serves N = 65..72.  The introgression (5,5)
+// model, N = 95: 421 against 461 M, so 81..96 stays VALU-only; other sizes unmeasured.)
 constexpr MCfg kMCfgs[] = {
     {33, 48, 3, 12, 1, 6, 0.35, false},   {49, 64, 4, 16, 1, 8, 0.35, false},
-    {65, 72, 5, 18, 1, 9, 0.35, false},   {73, 80, 5, 20, 1, 10, 0.35, false},
+    {65, 72, 5, 18, 1, 9, 0.35, true},    {73, 80, 5, 20, 1, 10, 0.35, false},
     {81, 96, 6, 24, 1, 12, 0.35, false},  {129, 136, 9, 34, 1, 17, 0.55, true},
     {137, 144, 9, 36, 1, 18, 0.55, true},
     // two groups per workgroup (experiment configuration, ITR_MCFG)

@@ -12,4 +12,7 @@ timeout -k 10 400 python bench.py $B > $O/bench_fv.json 2> $O/bench_fv.err || { 
 python scripts/bench_line.py $O/bench_fv.json chr10
 timeout -k 10 400 python bench.py $B --mode posterior --n-int 7 --steps 5 > $O/post77.json 2> $O/post77.err || { tail $O/post77.err; exit 1; }
 python scripts/bench_line.py $O/post77.json post77
+
+timeout -k 10 400 python bench.py $B --mode posterior --n-int 5 --steps 5 > $O/post55.json 2> $O/post55.err || { tail $O/post55.err; exit 1; }
+python scripts/bench_line.py $O/post55.json post55
 echo done
