@@ -47,4 +47,7 @@ timeout -k 10 300 python bench.py $B --mode optimize --steps 10 --warmup 3 > $O/
 python scripts/bench_line.py $O/opt55.json opt55
 timeout -k 10 300 python bench.py $B --dist 1 --backend nccl > $O/rccl1.json 2> $O/rccl1.err || { tail $O/rccl1.err; exit 1; }
 python scripts/bench_line.py $O/rccl1.json chr10_rccl_world1
+
+timeout -k 10 400 python bench.py $B --mode posterior --n-int 5 --steps 5 > $O/post55.json 2> $O/post55.err || { tail $O/post55.err; exit 1; }
+python scripts/bench_line.py $O/post55.json post55
 echo done
