@@ -495,12 +495,8 @@ void plan_partition(itr_plan_t p, const std::vector<int64_t>& ulen, int cus) {
   // two forward halves per reserved CU at a time when the one-per-CU set is large (more
   // than kFwdPairMin CUs), bins sized by the shared step kFwdPairStep
   int fpc = 1;
-  double fstep = kFwdPairStep;
-  int fmin = kFwdPairMin;
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_FWD_PAIR_STEP")) fstep = atof(getenv("ITR_FWD_PAIR_STEP"));
-  if (getenv("ITR_FWD_PAIR_MIN")) fmin = atoi(getenv("ITR_FWD_PAIR_MIN"));
-#endif
+  const double fstep = kFwdPairStep;
+  const int fmin = kFwdPairMin;
   if (rf > fmin) {
     const int rf2 = (ffd_bins(halves, T / fstep) + 1) / 2;
     if (rf2 < rf) {
@@ -1082,11 +1078,7 @@ int plan_create_impl(const int64_t* off, int64_t nblocks, double split_frac,
     std::vector<int64_t> gidx(ng);
     std::iota(gidx.begin(), gidx.end(), 0);
     std::stable_sort(gidx.begin(), gidx.end(), [&](int64_t x, int64_t y) { return gsteps[x] > gsteps[y]; });
-    double cf = kMixFwd, cv = kMixVit;
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_MIX_FWD")) cf = atof(getenv("ITR_MIX_FWD"));
-    if (getenv("ITR_MIX_VIT")) cv = atof(getenv("ITR_MIX_VIT"));
-#endif
+    const double cf = kMixFwd, cv = kMixVit;
     int64_t gi = 0, vi = p->vit_nlong;
     const int64_t nprio = kMixPrio;
     while (gi < ng || vi < nblocks) {
@@ -1851,11 +1843,7 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
     // matrix-core bulk of the backward launch.  (Splitting the forward sweep as well — a
     // forward + posterior sweep over [hi, T) in the backward launch — measured slower: 24.1
     // against 23.0 ms per (7,7) posterior, profiles/r5ps3_*.)
-    double bfrac = kPostBetaFrac, lofrac = kPostBetaLo;
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_POST_BETA_FRAC")) bfrac = atof(getenv("ITR_POST_BETA_FRAC"));
-    if (getenv("ITR_POST_BETA_LO")) lofrac = atof(getenv("ITR_POST_BETA_LO"));
-#endif
+    const double bfrac = kPostBetaFrac, lofrac = kPostBetaLo;
     // (split blocks are VALU tasks of the backward launch: a prefix of its VALU set, whose
     // limit mirrors run_hybrid's; their forward sweep is a VALU task or a matrix-core group)
     int64_t nurg = 0, nbeta = 0, brows = 0;

@@ -658,10 +658,6 @@ MfmaGeometry mfma_geometry(int n, int mode) {
   g.pfrac = kMCfgs[g.cfg].pfrac;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_POST_URGENT_FRAC")) g.pfrac = atof(getenv("ITR_POST_URGENT_FRAC"));
-  if (mode == MODE_FWD_STORE && getenv("ITR_POST_URGENT_FRAC_F"))
-    g.pfrac = atof(getenv("ITR_POST_URGENT_FRAC_F"));
-  if (mode == MODE_BWD && getenv("ITR_POST_URGENT_FRAC_B"))
-    g.pfrac = atof(getenv("ITR_POST_URGENT_FRAC_B"));
 #endif
   int occ = 1;
   (void)dispatch_mode_m(mode, g.cfg, false, nullptr, nullptr, 0, 0, nullptr, &occ);

@@ -1,4 +1,4 @@
-# same-box A/B over (library, settings) pairs: RUNS = "label|lib|VAR=v,VAR2=w ..." items
+# Same-box A/B over (library, settings) pairs: RUNS = "label|lib|VAR=v,VAR2=w ..." items
 # ("prod" = the product library), REPS rounds, one line per run into gpurun_out/$TAG/ab.txt
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

@@ -1,6 +1,7 @@
 """Kernel timeline of the last posterior call in a rocprofv3 kernel trace: start / end of
 every kernel launched after the last forward-store launch, relative to its start, with the
-queue each ran on and its grid (usage: ptimeline.py trace_kernel_trace.csv)."""
+queue each ran on and its grid.  usage: post_timeline.py <kernel_trace.csv> (a rocprofv3
+--kernel-trace of bench.py --mode posterior)."""
 import csv
 import sys
 

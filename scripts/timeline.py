@@ -1,5 +1,5 @@
 """Per-launch timeline of itr_forward_viterbi calls from a rocprofv3 kernel trace
-(scripts/r5/tl.sh): for each call (a run of launches between two fillBuffer/memset groups),
+(rocprofv3 --kernel-trace of bench.py --verify 0): for each call (a run of launches between two fillBuffer/memset groups),
 begin / end of every launch relative to the call's first launch, in ms, with its stream
 (queue) and grid.  usage: timeline.py <kernel_trace.csv> [calls=2]"""
 import csv
