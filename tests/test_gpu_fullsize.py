@@ -350,3 +350,37 @@ def test_short_blocks_133_pruned_viterbi(gpu):
     ll, path2 = hmm.forward_viterbi_device(model, plan, d_obs)
     assert np.array_equal(path2.cpu().numpy(), path)
     _check_all_blocks(build_tables(a, b, pi), obs, off, ll.cpu().numpy(), path)
+
+
+@pytest.mark.parametrize("golden_name,n", [("model_kat_5_5.npz", 70), ("model_kat_7_7.npz", 133)])
+def test_hybrid_posterior_split_blocks(gpu, golden_name, n):
+    """The matrix-core posterior's split of its longest blocks (itr_posterior: a beta-only
+    sweep over [lo, T) beside the forward launch, the backward launch's VALU task over
+    [0, lo] from the stored beta_lo, post_combine for (lo, T)) at N = 70 and N = 133, on a
+    mid-size layout: four long blocks (VALU tasks, split) among 700 short ones (matrix-core
+    groups; more than two blocks per CU, so the VALU-only concurrent split does not take
+    it).  Every row against the CPU restatement (1e-8) and against the same plan without
+    the split (post_split_frac=0: the long blocks' whole backward + posterior sweep in the
+    backward launch), 1e-12."""
+    import torch
+    g = golden(golden_name)
+    a, b, pi = g["a"], g["b"], g["pi"]
+    assert a.shape[0] == n
+    short = block_lengths(np.random.default_rng(21), 210_000, 300.0)
+    lengths = np.concatenate([[6000, 5200, 4700, 5600], short]).astype(np.int64)
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=901)
+    assert len(lengths) > 2 * 256 + 4
+    model = hmm.Model(a, b, pi)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).cuda()
+    plan = hmm.Plan(off)
+    plan.reserve(n, posterior=True)
+    post = hmm.posterior_device(model, plan, d_obs)
+    plan0 = hmm.Plan(off, post_split_frac=0)
+    plan0.reserve(n, posterior=True)
+    post0 = hmm.posterior_device(model, plan0, d_obs)
+    np.testing.assert_allclose(post.cpu().numpy(), post0.cpu().numpy(), rtol=1e-12, atol=1e-300)
+    assert float((post.sum(dim=1) - 1.0).abs().max()) < 1e-12
+    t = build_tables(a, b, pi)
+    assert _posterior_every_block(t, obs, off, post, chunk_cols=100_000) == off[-1]
+    del post, post0, d_obs
+    torch.cuda.empty_cache()
