@@ -234,13 +234,27 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
       // lanes read column 0: finite, and their products are 0); a backward half's last step
       // (a row of ones) is applied where the value is used.  A clamp or a select on a fresh
       // load makes hipcc wait for it on the spot (s_waitcnt vmcnt(0) every column).
+      // (posterior modes: addresses as a per-row base plus one 32 x 32 -> 64-bit product with
+      // the byte stride — v_mad_u64_u32 with the base as addend — instead of 64-bit index
+      // arithmetic per load: (7,7) posterior 22.17-22.24 -> 22.11-22.16 ms; the forward
+      // log-likelihood sweep keeps the index form, 4.00-4.04 against 4.02-4.11 ms with it,
+      // profiles/r5abaddr_ab.txt)
+      const uint16_t* obr[GB];
+#pragma unroll
+      for (int gb = 0; gb < GB; ++gb) obr[gb] = p.obs + (Tb[gb] > 0 ? c0[gb] : 0);
       auto sym = [&](int gb, int s) -> int {
         const int t = dir[gb] > 0 ? s : Tb[gb] - 1 - s;
         const int tc = min(max(t, 0), max(Tb[gb] - 1, 0));
-        return (int)p.obs[Tb[gb] > 0 ? c0[gb] + tc : 0];
+        if constexpr (MODE == MODE_FWD_LL) return (int)p.obs[Tb[gb] > 0 ? c0[gb] + tc : 0];
+        return (int)obr[gb][(uint32_t)tc];
       };
       const int jc = jv ? j : 0;
-      auto emis = [&](int sy) -> double { return p.emit[min(sy, 624) * n + jc]; };
+      const char* const ebase = reinterpret_cast<const char*>(p.emit + jc);
+      const uint32_t rowb = (uint32_t)n * 8u;  // bytes per emission row
+      auto emis = [&](int sy) -> double {
+        if constexpr (MODE == MODE_FWD_LL) return p.emit[min(sy, 624) * n + jc];
+        return *reinterpret_cast<const double*>(ebase + (uint64_t)(uint32_t)min(sy, 624) * rowb);
+      };
       auto ones_at = [&](int gb, int s) -> bool {
         return MODE == MODE_FWD_LL && task_split[gb] < 0 && s == T[gb] - 1;
       };
@@ -315,7 +329,10 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
                   }
                 } else {
                   // past the row's end: the lane's sink slot (a select, not a branch)
-                  double* dst = t < T[gb] ? p.alpha + (c0[gb] + t) * p.astride + j : sink;
+                  double* dst = t < T[gb] ? reinterpret_cast<double*>(
+                                                  reinterpret_cast<char*>(p.alpha + c0[gb] * p.astride + j) +
+                                                  (uint64_t)(uint32_t)t * ((uint32_t)p.astride * 8u))
+                                            : sink;
                   *dst = x[gb];
                 }
                 if (jv) X[gb][buf ^ 1][r][j] = x[gb];
@@ -389,14 +406,14 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
           ab[gb] = p.alpha + cb * p.astride + j;
           pb[gb] = p.post + cb * n + j;
         }
-        const double* eb = p.emit + jc;
-        const uint32_t ast = (uint32_t)p.astride, un = (uint32_t)n;
+        const uint32_t ast8 = (uint32_t)p.astride * 8u, un8 = (uint32_t)n * 8u;  // byte strides
         auto bsym = [&](int gb, int s) -> int {  // symbol of column T-1-s
-          return (int)ob[gb][max(T[gb] - 1 - s, 0)];
+          return (int)ob[gb][(uint32_t)max(T[gb] - 1 - s, 0)];
         };
-        auto bemis = [&](int sy) -> double { return eb[(uint64_t)(uint32_t)min(sy, 624) * un]; };
+        auto bemis = [&](int sy) -> double { return emis(sy); };
         auto arow = [&](int gb, int s) -> double {  // stored forward row of column T-1-s
-          return ab[gb][(uint64_t)(uint32_t)max(T[gb] - 1 - s, 0) * ast];
+          return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(ab[gb]) +
+                                                  (uint64_t)(uint32_t)max(T[gb] - 1 - s, 0) * ast8);
         };
 #pragma unroll
         for (int gb = 0; gb < GB; ++gb) {
@@ -467,7 +484,8 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
               }
               const int sp = s - 2;  // the column of step s - 2
               double* dst = (sp >= 0 && sp < T[gb] && jv)
-                                ? pb[gb] + (uint64_t)(uint32_t)(T[gb] - 1 - sp) * un
+                                ? reinterpret_cast<double*>(reinterpret_cast<char*>(pb[gb]) +
+                                                            (uint64_t)(uint32_t)(T[gb] - 1 - sp) * un8)
                                 : sink;
               *dst = q2[gb] * rn[gb];
               q2[gb] = q1[gb];
