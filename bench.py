@@ -163,15 +163,29 @@ def valu_peaks():
     return fma, am, os.path.relpath(files[-1], ROOT)
 
 
+def summary_files():
+    """profiles/r*_summary.json, the one recorded for this build of the library first (its
+    `library_sha256` entry, written when it was copied in), then by round tag, newest first."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")), reverse=True)
+    h = lib_sha256()
+
+    def this_build(f):
+        try:
+            return json.load(open(f)).get("library_sha256") == h
+        except (OSError, ValueError):
+            return False
+    return sorted(files, key=lambda f: not this_build(f))  # (stable: tag order kept)
+
+
 def pmc_traffic(n, mode, tag_hint=""):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
     of this command (scripts/gpu_round.sh -> scripts/summarize_profile.py ->
     profiles/*_summary.json: FETCH_SIZE + WRITE_SIZE from separate passes, raw)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))  # by round tag
-    for f in reversed(files):
+    for f in summary_files():
         d = json.load(open(f))
         if mode == 3:  # Viterbi: the long-block sweep and the per-wave sweep of one call
-            parts = [(k, v) for k, v in d.items() if v.get("n_states", 70) == n and
+            parts = [(k, v) for k, v in d.items() if isinstance(v, dict) and
+                     v.get("n_states", 70) == n and
                      "hbm_bytes_raw" in v and ("wave_vit_kernel" in k or
                                                (k.startswith("void itr::sweep_kernel<") and
                                                 k.endswith(", 3>(itr::SweepArgs)")))]
@@ -187,6 +201,8 @@ def pmc_traffic(n, mode, tag_hint=""):
                     "): 2 x FETCH_SIZE + WRITE_SIZE per call (all launches of each kernel; "
                     "gfx950 FETCH correction)")
         for name, v in d.items():
+            if not isinstance(v, dict):
+                continue
             hyb = re.search(r"hybrid_sweep_kernel<\d+, \d+, \d+, (\d+),", name)
             if ((name.startswith("void itr::sweep_kernel<") and
                  name.endswith(f", {mode}>(itr::SweepArgs)")) or
@@ -213,13 +229,15 @@ def fv_call_traffic():
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_fv_call_traffic.json")))
     if not files:
         return None, "no per-call PMC traffic under profiles/"
-    d = json.load(open(files[-1]))
-    name = os.path.basename(files[-1])
-    if d.get("library_sha256") != lib_sha256():
-        return None, (f"{name} was profiled on another build of the library (not this one): "
-                      "no traffic for this build")
-    return d["bytes_per_call"], (f"{name}: 2 x FETCH_SIZE + WRITE_SIZE of every launch of the "
-                                 f"call ({len(d['per_kernel'])} kernels), this build")
+    h = lib_sha256()
+    for f in reversed(files):  # the profile of this build, whatever its tag sorts as
+        d = json.load(open(f))
+        if d.get("library_sha256") == h:
+            return d["bytes_per_call"], (
+                f"{os.path.basename(f)}: 2 x FETCH_SIZE + WRITE_SIZE of every launch of the "
+                f"call ({len(d['per_kernel'])} kernels), this build")
+    return None, (f"none of the {len(files)} profiles/r*_fv_call_traffic.json ran this build of "
+                  "the library: no traffic for this build")
 
 
 def pmc_rates(n):
@@ -229,12 +247,11 @@ def pmc_rates(n):
     work issued (SQ_INSTS_VALU x 4 cycles), as shares of all SIMDs of the chip over the
     launch's duration (a launch on a CU subset scores its share of the whole chip), plus the
     waves' waitcnt share (SQ_WAIT_ANY / SQ_WAVE_CYCLES)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")))
-    for f in reversed(files):
+    for f in summary_files():
         d = json.load(open(f))
         out = {}
         for name, v in d.items():
-            if v.get("n_states", 70) != n or "mfma_util" not in v or \
+            if not isinstance(v, dict) or v.get("n_states", 70) != n or "mfma_util" not in v or \
                     not ("sweep_kernel" in name or "wave_" in name):
                 continue
             share = 1.0  # shares of all SIMDs of the chip (launches run on CU subsets)

@@ -71,10 +71,16 @@ def main(prof_dir, out, subs):
         # state count of the profiled launch: the (7,7) model's kernels carry NT = 9 tiles
         e["n_states"] = 133 if ("<9, 34," in k or "<9, 36," in k) else 70
         res[k] = e
-    json.dump(res, open(out, "w"), indent=1)
     for k, e in res.items():
         print(k[:100])
         print("   ", {x: y for x, y in e.items() if x != "counters"})
+    # the library the profiled command loaded (bench.py prefers the summary of its own build)
+    lib = os.environ.get("ITR_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                     "..", "itrails_amd", "libitrails_hip.so")
+    if os.path.exists(lib):
+        import hashlib
+        res["library_sha256"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    json.dump(res, open(out, "w"), indent=1)
 
 
 if __name__ == "__main__":
