@@ -300,13 +300,16 @@ struct itr_plan {
   // split set cached in sublo_key (nbeta, first split column fraction)
   int64_t* d_sublo = nullptr;
   std::pair<int64_t, double> sublo_key{-1, 0.0};
+  int64_t* d_comb = nullptr;  // their combine tasks {block, t0, t1} (columns (lo, T))
+  int64_t ncomb = 0;
   double* d_beta = nullptr;
   size_t beta_cap = 0;
   int32_t* d_order = nullptr;
   int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep,
                            // [3, 4] hybrid sweeps, [5, 6] Viterbi hybrid, [7] per-wave Viterbi,
                            // [8, 9] the idle loop of a split hybrid launch, [10] per-wave forward,
-                           // [12] mixed launch, [13] the long blocks' traceback
+                           // [12] mixed launch, [13] the long blocks' traceback, [14] the
+                           // posterior's combine tasks
   double* d_sink = nullptr;  // write target of padded states (64 doubles per workgroup,
                              // itr::kSinkWgs of them)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
@@ -638,6 +641,7 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
 // backward sweep beside their forward one (itr_posterior)
 constexpr double kPostBetaFrac = 0.5;
 constexpr double kPostBetaLo = 0.4;  // their split column, as a fraction of their length
+constexpr int64_t kCombCols = 256;     // columns per combine task of the backward launch
 
 // nbeta (posterior, forward-store launch): the first nbeta blocks of the order also get a
 // backward task storing beta rows into v.beta (over [v.sub_lo[block], T)).
@@ -1185,6 +1189,7 @@ int itr_plan_destroy(itr_plan_t p) {
   dev_free(p->d_tile_off);
   dev_free(p->d_boff);
   dev_free(p->d_sublo);
+  dev_free(p->d_comb);
   dev_free(p->d_beta);
   dev_free(p->d_order);
   dev_free(p->d_queue);
@@ -1857,12 +1862,22 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
     if (nbeta > 0 && p->sublo_key != std::make_pair(nbeta, lofrac)) {
       if (!p->d_sublo)
         if (int e = dev_alloc(&p->d_sublo, p->nblocks)) return e;
-      std::vector<int64_t> lo(p->nblocks, 0);
-      for (int64_t k = 0; k < nbeta; ++k)  // (blocks >= 512 columns)
-        lo[p->h_order[k]] = std::clamp<int64_t>((int64_t)(lofrac * (double)p->sorted_len[k]), 1,
-                                                p->sorted_len[k] - 2);
+      std::vector<int64_t> lo(p->nblocks, 0), comb;
+      for (int64_t k = 0; k < nbeta; ++k) {  // (blocks >= 512 columns)
+        const int64_t T = p->sorted_len[k];
+        const int64_t l = std::clamp<int64_t>((int64_t)(lofrac * (double)T), 1, T - 2);
+        lo[p->h_order[k]] = l;
+        for (int64_t t0 = l + 1; t0 < T; t0 += kCombCols)  // combine tasks of (lo, T)
+          comb.insert(comb.end(), {p->h_order[k], t0, std::min(T, t0 + kCombCols)});
+      }
       HIP_TRY(hipMemcpy(p->d_sublo, lo.data(), lo.size() * sizeof(int64_t),
                         hipMemcpyHostToDevice));
+      dev_free(p->d_comb);
+      p->d_comb = nullptr;
+      if (int e = dev_alloc(&p->d_comb, comb.size())) return e;
+      HIP_TRY(hipMemcpy(p->d_comb, comb.data(), comb.size() * sizeof(int64_t),
+                        hipMemcpyHostToDevice));
+      p->ncomb = (int64_t)comb.size() / 3;
       p->sublo_key = {nbeta, lofrac};
     }
     if (nbeta > 0 && (size_t)brows * g.xr > p->beta_cap) {
@@ -1882,14 +1897,16 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
     a.post = post;
     a.beta = nullptr;
     a.beta_in = nbeta > 0 ? p->d_beta : nullptr;
-    if (int e = run_hybrid(itr::MODE_BWD, m, p, a, gb, st, "posterior_bwd")) return e;
-    // (post_combine beside the backward launch, on a side stream, delayed that launch's
-    // workgroups by as much as it saved: 22.25 against 22.18 ms, profiles/r5ptl3_*)
-    if (nbeta > 0)
-      HIP_TRY(itr::launch_post_combine(m->n, g.xr, (int)nbeta, p->sorted_len[0], p->d_order,
-                                       p->d_off, p->d_alpha, p->d_beta, p->d_boff, post, st,
-                                       p->d_sublo));
-    return 0;
+    // the combine of (lo, T) as tasks at the end of the backward launch's queue (a launch of
+    // its own after it: 0.2-0.27 ms; beside it on a side stream it delayed that launch's
+    // workgroups by as much as it saved, profiles/r5ptl3_*)
+    if (nbeta > 0) {
+      a.comb = p->d_comb;
+      a.ncomb = p->ncomb;
+      a.comb_queue = p->d_queue + 14;
+      HIP_TRY(hipMemsetAsync(a.comb_queue, 0, sizeof(int), st));
+    }
+    return run_hybrid(itr::MODE_BWD, m, p, a, gb, st, "posterior_bwd");
   }
   const int nl = (int)p->npsplit;
   if (post_split_path(m->n, p)) {

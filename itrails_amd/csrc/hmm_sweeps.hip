@@ -298,18 +298,8 @@ __global__ void __launch_bounds__(256) post_combine_kernel(int n, int xr, const 
   const int64_t lo = sub_lo ? sub_lo[blk] : 0;  // first column with a beta row
   const int64_t t = (sub_lo ? lo + 1 : 0) + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T) return;
-  const int l = threadIdx.x & 63;
-  const double* a = alpha + (c0 + t) * xr;
-  const double* b = beta + (beta_off[blk] + t - lo) * xr;
-  const double q0 = l < n ? a[l] * b[l] : 0.0;
-  const double q1 = l + 64 < n ? a[l + 64] * b[l + 64] : 0.0;
-  const double q2 = l + 128 < n ? a[l + 128] * b[l + 128] : 0.0;  // (n <= 192)
-  const double S = wave_sum((q0 + q1) + q2);
-  const double rS = 1.0 / S;
-  double* dst = post + (c0 + t) * n;
-  if (l < n) dst[l] = q0 * rS;
-  if (l + 64 < n) dst[l + 64] = q1 * rS;
-  if (l + 128 < n) dst[l + 128] = q2 * rS;
+  post_combine_column(n, xr, alpha + (c0 + t) * xr, beta + (beta_off[blk] + t - lo) * xr,
+                      post + (c0 + t) * n, threadIdx.x & 63);
 }
 
 hipError_t launch_post_combine(int n, int xr, int nlong, int64_t tmax, const int32_t* order,

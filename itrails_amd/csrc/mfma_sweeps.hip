@@ -562,6 +562,26 @@ __global__ void __launch_bounds__(64 * NT, (MOcc<NT, NK, GB, MODE>::value))
     if (g0 >= p.ngroups) break;
     mfma_task<NT, NK, GB, MODE>(p, smem, g0);
   }
+  // the split blocks' combine (posterior rows of (lo, T) from the stored rows), taken by the
+  // workgroups that run out of groups: it fills the launch's tail instead of a launch of its
+  // own after it
+  if constexpr (MODE == MODE_BWD) {
+    for (;;) {
+      if (threadIdx.x == 0) qslot[0] = v.ncomb > 0 ? atomicAdd(v.comb_queue, 1) : 0;
+      lds_barrier();
+      const int ci = uni(qslot[0]);
+      lds_barrier();
+      if (ci >= v.ncomb) break;
+      const int blk = (int)v.comb[3 * ci];
+      const int64_t c0 = v.off[blk], lo = v.sub_lo[blk];
+      const int64_t t1 = v.comb[3 * ci + 2];
+      const int xr = 16 * NT;
+      for (int64_t t = v.comb[3 * ci + 1] + (threadIdx.x >> 6); t < t1; t += NT)
+        post_combine_column(v.n, xr, v.alpha + (c0 + t) * xr,
+                            v.beta_in + (v.beta_off[blk] + t - lo) * xr, v.post + (c0 + t) * v.n,
+                            threadIdx.x & 63);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------

@@ -54,6 +54,10 @@ struct SweepArgs {
                                 //   only, storing beta_lo .. beta_{T-1}; a posterior task
                                 //   sweeps columns [0, lo] only, from beta_lo (beta_in)
   const double* beta_in;        //   the stored beta rows the posterior tasks start from
+  const int64_t* comb;          // hybrid MODE_BWD: ncomb combine tasks {block, t0, t1}: the
+  int64_t ncomb;                //   posterior rows of columns [t0, t1) from the stored alpha
+  int* comb_queue;              //   and beta rows (the split blocks' (lo, T)), after the
+                                //   matrix-core groups; their work counter
   const int32_t* tasks;         // MODE_FWD_LL: [nblocks x 3] {block, split, slot}, see capi.cpp
   double* svec;                 // MODE_FWD_LL: [nsplit x 2 x XR] vectors of split blocks
   int* sK;                      // MODE_FWD_LL: [nsplit x 2] their power-of-two exponents

@@ -199,6 +199,22 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
+// One posterior row from stored alpha and beta rows, by one wave (lane l: states l, l + 64,
+// l + 128; n <= 192): alpha * beta / sum_j alpha_j beta_j, the backward sweep's expression
+// (optimizer.py:228-238).  post_combine_kernel and the backward hybrid launch's combine tasks.
+__device__ __forceinline__ void post_combine_column(int n, int xr, const double* a,
+                                                    const double* b, double* dst, int l) {
+  (void)xr;
+  const double q0 = l < n ? a[l] * b[l] : 0.0;
+  const double q1 = l + 64 < n ? a[l + 64] * b[l + 64] : 0.0;
+  const double q2 = l + 128 < n ? a[l + 128] * b[l + 128] : 0.0;
+  const double S = wave_sum((q0 + q1) + q2);
+  const double rS = 1.0 / S;
+  if (l < n) dst[l] = q0 * rS;
+  if (l + 64 < n) dst[l + 64] = q1 * rS;
+  if (l + 128 < n) dst[l + 128] = q2 * rS;
+}
+
 // s_waitcnt vmcnt(0) (expcnt/lgkmcnt untouched).  Issued once before each step loop so
 // that no loop-carried register is the destination of a load in flight at loop entry:
 // otherwise hipcc's waitcnt pass puts a vmcnt(0) INSIDE the loop at that register's first
