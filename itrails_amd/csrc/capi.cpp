@@ -308,8 +308,8 @@ struct itr_plan {
   int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep,
                            // [3, 4] hybrid sweeps, [5, 6] Viterbi hybrid, [7] per-wave Viterbi,
                            // [8, 9] the idle loop of a split hybrid launch, [10] per-wave forward,
-                           // [12] mixed launch, [13] the long blocks' traceback, [14] the
-                           // posterior's combine tasks
+                           // [12] mixed launch, [13] the long blocks' traceback; the hybrid
+                           // posterior: [3, 4] forward-store, [5, 6] backward, [7] combine
   double* d_sink = nullptr;  // write target of padded states (64 doubles per workgroup,
                              // itr::kSinkWgs of them)
   int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
@@ -648,7 +648,7 @@ constexpr int64_t kCombCols = 256;     // columns per combine task of the backwa
 int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const itr::MfmaGeometry& g,
                hipStream_t st, const char* tname, bool valu = true, bool mfma = true,
                int64_t max_grid = -1, bool zero_queues = true, int cus = 0,
-               bool share_cu = false, int64_t nbeta = 0) {
+               bool share_cu = false, int64_t nbeta = 0, int qbase = 3) {
   if (cus <= 0) cus = cu_count();
   itr::MfmaArgs a{};
   a.n = m->n;
@@ -668,7 +668,7 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   a.matT = m->aT;
   a.svec = p->d_svec;
   a.sK = p->d_sK;
-  a.queue = p->d_queue + 4;
+  a.queue = p->d_queue + qbase + 1;
   a.off = p->d_off;
   a.obs = v.obs;
   a.mat = m->a;
@@ -680,7 +680,7 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   a.post = v.post;
   a.sink = v.sink;
   a.prio_len = INT32_MAX;
-  v.queue = p->d_queue + 3;
+  v.queue = p->d_queue + qbase;
   v.prio_len = 0;  // every VALU task of the hybrid is a long block: raised wave priority
   // a part launched alone takes the other part's loop through a counter of its own (the
   // real counter belongs to the concurrent launch of that part)
@@ -704,7 +704,7 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   itr::MfmaGeometry gx = g;
   // one workgroup per CU (unless the caller packs several VALU tasks per CU: share_cu)
   if (grid <= cus && !share_cu) gx.lds_min = itr::kExclusiveLds;
-  if (zero_queues) HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
+  if (zero_queues) HIP_TRY(hipMemsetAsync(p->d_queue + qbase, 0, 2 * sizeof(int), st));
 #ifdef ITR_DIAG
   if (getenv("ITR_VERBOSE"))
     fprintf(stderr, "[itr] %s hybrid: n=%d cfg=%d block=%d per_cu=%d grid=%lld valu=%lld groups=%lld\n",
@@ -1891,8 +1891,11 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
       a.beta_off = p->d_boff;
       a.sub_lo = p->d_sublo;
     }
+    // the two launches' work counters ([3, 4] forward, [5, 6] backward) and the combine
+    // tasks' ([7]) zeroed by one memset up front
+    HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 5 * sizeof(int), st));
     if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, st, "posterior_fwd", true, true, -1,
-                           true, 0, false, nbeta))
+                           false, 0, false, nbeta))
       return e;
     a.post = post;
     a.beta = nullptr;
@@ -1903,10 +1906,10 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
     if (nbeta > 0) {
       a.comb = p->d_comb;
       a.ncomb = p->ncomb;
-      a.comb_queue = p->d_queue + 14;
-      HIP_TRY(hipMemsetAsync(a.comb_queue, 0, sizeof(int), st));
+      a.comb_queue = p->d_queue + 7;
     }
-    return run_hybrid(itr::MODE_BWD, m, p, a, gb, st, "posterior_bwd");
+    return run_hybrid(itr::MODE_BWD, m, p, a, gb, st, "posterior_bwd", true, true, -1, false, 0,
+                      false, 0, 5);
   }
   const int nl = (int)p->npsplit;
   if (post_split_path(m->n, p)) {
