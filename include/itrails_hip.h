@@ -156,8 +156,11 @@ ITR_API int itr_posterior(itr_model_t model, itr_plan_t plan, const uint16_t* d_
  * (blocks[k], lens[k] columns; read_data.py:94-117), which must match the plan's layout.
  * The blocks are packed and range-checked by host threads into a pinned buffer (ITR_EDATA
  * for a symbol outside the 625-letter alphabet, like the reference's IndexError), copied to
- * a device buffer kept by the calling thread (itr_release_staging frees both), swept on the
- * null stream, and the results returned to host memory:
+ * a device buffer kept by the calling thread (itr_release_staging frees both; so does the
+ * thread's exit), and swept on the calling thread's own non-blocking stream, which first
+ * waits for the work already queued on the null stream (so a sweep of the same plan queued
+ * there finishes first).  Work on other streams that uses the same plan must be synchronised
+ * by the caller.  The results are returned to host memory:
  *   itr_forward_loglik_blocks: h_loglik[k] = forward_loglik of block k (optimizer.py:145-162)
  *   itr_viterbi_blocks:        h_path[c]  = Viterbi state of column c as float64, the dtype
  *                              backtrack_viterbi returns (optimizer.py:336-377)

@@ -8,7 +8,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["hmm_sweeps.hip", "mfma_sweeps.hip", "wave_sweeps.hip", "dense.hip", "vanloan.hip", "emission.hip", "rows.hip", "prune_vit.hip", "maf.cpp", "writers.cpp", "capi.cpp"]
+SOURCES = ["hmm_sweeps.hip", "mfma_sweeps.hip", "wave_sweeps.hip", "dense.hip", "vanloan.hip", "emission.hip", "rows.hip", "prune_vit.hip", "maf.cpp", "writers.cpp", "planner.cpp", "host_io.cpp", "capi.cpp"]
 OUT = os.path.join(HERE, "libitrails_hip.so")
 # The sweeps never produce NaN (log 0 = -inf is the only non-finite value, and no
 # inf - inf or 0/0 is formed), so fmax needs no NaN-quieting canonicalize after each DPP

@@ -1,33 +1,12 @@
 // capi.cpp — the C ABI declared in include/itrails_hip.h: object lifetimes, argument
 // checking, workspace management and kernel launches.  No compute happens on the host.
-#include <hip/hip_runtime.h>
+#include "capi_internal.h"
 
-#include <algorithm>
-#include <cstdarg>
-#include <cstdio>
-#include <cstdlib>
-#include <cmath>
-#include <cstring>
-#include <deque>
-#include <mutex>
-#include <numeric>
-#include <optional>
-#include <atomic>
-#include <string>
-#include <chrono>
-#include <thread>
-#include <tuple>
-#include <vector>
-
-#include "../../include/itrails_hip.h"
-#include "dense.h"
-#include "maf.h"
-#include "writers.h"
-#include "sweeps.h"
+namespace itr_host {
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -39,29 +18,11 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-// host threads of this job: OMP_NUM_THREADS when set (the GPU pool sets it to the job's CPU
-// share), else the machine's cores; at most 16
-int host_threads() {
-  const char* e = getenv("OMP_NUM_THREADS");
-  int n = e ? atoi(e) : 0;
-  if (n <= 0) n = (int)std::thread::hardware_concurrency();
-  return std::max(1, std::min(16, n));
-}
-template <class F>
-void parallel_for(int nt, F&& f) {
-  std::vector<std::thread> th;
-  for (int w = 1; w < nt; ++w) th.emplace_back(f, w);
-  f(0);
-  for (auto& t : th) t.join();
-}
+}  // namespace itr_host
 
-#define HIP_TRY(expr)                                                                      \
-  do {                                                                                     \
-    hipError_t e_ = (expr);                                                                \
-    if (e_ != hipSuccess)                                                                  \
-      return fail(ITR_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),         \
-                  __FILE__, __LINE__);                                                     \
-  } while (0)
+using namespace itr_host;
+
+namespace {
 
 // ---- per-thread kernel timing (HIP events on the launch stream) -----------------------
 struct Timer {
@@ -107,13 +68,6 @@ struct Scope {
   }
 };
 
-int cu_count() {
-  int dev = 0, n = 0;
-  (void)hipGetDevice(&dev);
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    n = 256;
-  return n > 0 ? n : 256;
-}
 
 // Two CU-masked streams per device and host thread: `lng` on `reserve` CUs spread over the
 // device, `blk` on the others, plus fork / join events.  itr_viterbi decodes the longest
@@ -247,136 +201,9 @@ int partition(int reserve, int reserve2, Partition** out, bool masked = true) {
   return 0;
 }
 
-template <class T>
-int dev_alloc(T** p, size_t count) {
-  *p = nullptr;
-  if (count == 0) count = 1;
-  HIP_TRY(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
-  return 0;
-}
-template <class T>
-void dev_free(T*& p) {
-  if (p) (void)hipFree(p);
-  p = nullptr;
-}
-
 }  // namespace
 
-struct itr_model {
-  int device = 0;
-  int n = 0;
-  double *a = nullptr, *la = nullptr, *E = nullptr, *LE = nullptr, *PIE = nullptr,
-         *LPIE = nullptr, *aT = nullptr;
-  // the one-block-per-wave Viterbi (wave_tasks.h), when that layout serves this state count
-  // (xrw = its slot count): log E padded to xrw columns (-inf) by state (the full-scan step)
-  // and in the bound-pruned step's slot order, the state of every slot, max_{i != j} log a_ij
-  // per slot; built on the model's first Viterbi call (vit_slot_tables) from host copies of
-  // the tables kept until then
-  double* LEW = nullptr;
-  double* LEWP = nullptr;
-  int32_t* VSLOT = nullptr;
-  double* VMB = nullptr;
-  double* MJ = nullptr;  // [n] max_{i != j} log a_ij (the bound-pruned Viterbi, prune_vit.hip)
-  int xrw = 0;
-  std::vector<double> h_a, h_la, h_LE, h_E, h_PIE;  // (E, PIE: the 256 N-free symbols)
-  std::mutex vit_mu;  // (the first Viterbi calls of several threads)
-  // E padded to the per-wave matrix-core forward's width (zero columns) plus a row of ones
-  // (row 625), when that layout serves this state count (wave_tasks.h)
-  double* EF = nullptr;
-  int erf = 0;
-};
-
-struct itr_plan {
-  int device = 0;
-  int64_t nblocks = 0, total = 0;
-  int64_t ntiles = 0;            // Viterbi tile records: sum over blocks of ceil(T / 16)
-  int64_t* d_off = nullptr;
-  int64_t* d_tile_off = nullptr;  // [nblocks+1] first tile record of every block
-  // posterior split (launch_post_split): the first npsplit blocks of the order get their
-  // backward sweep concurrently with the forward one; beta rows at d_boff[block]
-  int64_t npsplit = 0, beta_rows = 0;
-  int64_t* d_boff = nullptr;
-  // hybrid posterior: per-block split column of the longest blocks (0: not split), for the
-  // split set cached in sublo_key (nbeta, first split column fraction)
-  int64_t* d_sublo = nullptr;
-  std::pair<int64_t, double> sublo_key{-1, 0.0};
-  int64_t* d_comb = nullptr;  // their combine tasks {block, t0, t1} (columns (lo, T))
-  int64_t ncomb = 0;
-  double* d_beta = nullptr;
-  size_t beta_cap = 0;
-  int32_t* d_order = nullptr;
-  int* d_queue = nullptr;  // work counters: [0] fwd/bwd sweeps, [1] traceback, [2] Viterbi sweep,
-                           // [3, 4] hybrid sweeps, [5, 6] Viterbi hybrid, [7] per-wave Viterbi,
-                           // [8, 9] the idle loop of a split hybrid launch, [10] per-wave forward,
-                           // [12] mixed launch, [13] the long blocks' traceback; the hybrid
-                           // posterior: [3, 4] forward-store, [5, 6] backward, [7] combine
-  double* d_sink = nullptr;  // write target of padded states (64 doubles per workgroup,
-                             // itr::kSinkWgs of them)
-  int prio_len = INT32_MAX;  // length of the ~CU-count-th longest block
-  std::vector<int64_t> sorted_len;  // block lengths, longest first (processing order)
-  std::vector<int64_t> h_off;       // block offsets (host copy: the host-block entry points)
-  std::vector<int32_t> h_order;     // processing order (host copy of d_order)
-  // forward log-likelihood tasks {block, split, slot} (split blocks: two halves) and the
-  // split blocks' scratch
-  int64_t ntasks = 0, nsplit = 0;
-  int32_t *d_tasks = nullptr, *d_split_blk = nullptr;
-  // hybrid (matrix-core) sweeps, see itr_plan_create: forward log-likelihood = VALU tasks
-  // utasks + matrix-core groups of task ids into mtasks (split slots hsplit_blk); posterior =
-  // VALU blocks order[0, nurg) + groups of four consecutive blocks of order[nurg, nblocks),
-  // nurg chosen per call from the state count (MfmaGeometry.pfrac)
-  // per-wave matrix-core forward (wave_tasks.h): groups of four ids of `tasks`
-  int64_t nwgroups = 0;
-  int32_t* d_wgroups = nullptr;
-  // Viterbi placement (viterbi_impl): the vit_nlong longest blocks (vit_long_cols columns)
-  // on the 9-wave layout; the combined call's mixed queue (wave_sweeps.hip): entries >= 0 =
-  // Viterbi blocks, < 0 = forward groups of groups_ll, by expected duration; tasks at least
-  // mix_prio_* long run at raised wave priority
-  int64_t vit_nlong = 0, vit_long_cols = 0, nmix = 0;
-  int64_t vit_nlong_v = 0;  // the Viterbi-only call's long set (plan_partition)
-  // CU partition (plan_partition): reserved CUs for the long blocks' Viterbi and for the
-  // forward's VALU halves; wave_ok = false when the long work cannot fit half the chip
-  int vit_reserve = 0, fwd_reserve = 0;
-  int long_per_cu = 1;  // long Viterbi blocks a reserved CU sweeps at a time
-  int fwd_per_cu = 1;   // forward VALU halves a reserved CU sweeps at a time
-  bool wave_ok = true;
-  int32_t* d_mix = nullptr;
-  int mix_prio_fwd = INT32_MAX, mix_prio_vit = INT32_MAX;
-  // per-wave Viterbi: blocks shorter than this take the bound-pruned step (wave_tasks.h), in
-  // the forward+Viterbi and the Viterbi-only call
-  int vit_prune_len = 0, vit_prune_len_v = 0;
-  int64_t prune_override = -1;  // itr_plan_set_prune_len (negative: the planned lengths)
-  int64_t nutasks = 0, ngroups_ll = 0, nhsplit = 0;
-  int32_t *d_utasks = nullptr, *d_mtasks = nullptr, *d_groups_ll = nullptr,
-          *d_hsplit_blk = nullptr;
-  double* d_svec = nullptr;
-  int* d_sK = nullptr;
-  // workspace (grown on demand): forward rows (posterior) or the Viterbi checkpoint rows,
-  // and the Viterbi stay-flag words
-  uint16_t* d_stay = nullptr;
-  size_t stay_cap = 0;
-  uint8_t* d_last = nullptr;
-  double* d_alpha = nullptr;
-  size_t alpha_cap = 0;
-};
-
 namespace {
-
-int check_model(itr_model_t m) {
-  if (!m) return fail(ITR_EINVAL, "null model");
-  int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  if (dev != m->device)
-    return fail(ITR_ESTATE, "model lives on device %d, current device is %d", m->device, dev);
-  return 0;
-}
-int check_plan(itr_plan_t p) {
-  if (!p) return fail(ITR_EINVAL, "null plan");
-  int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  if (dev != p->device)
-    return fail(ITR_ESTATE, "plan lives on device %d, current device is %d", p->device, dev);
-  return 0;
-}
 
 // Workspace: Viterbi = one checkpoint row (f64) and one flag word (u16) per state per
 // 16-column tile record; posterior = the forward rows of every column.
@@ -385,168 +212,30 @@ int vit_stride(int n) {
   return wv.iq > 0 ? wv.xr : itr::sweep_row_stride(n, itr::MODE_VIT);
 }
 
-// Per-column costs of the sweep layouts of the (5,5) model (N = 65..72, the only state counts
-// with the per-wave layouts), measured on MI355X (profiles/r3l_*, r3u_*):
-//   kVitLone    a Viterbi block alone on its CU, 9-wave VALU layout           325 ns / column
-//   kVitWaveLat a per-wave Viterbi block's step under full load (latency)      800 ns / column
-//   kBulkCu     forward + Viterbi of a column in the mixed per-wave launch     180 CU-ns / column
-//               (calibrated on chr10: 0.15 / 0.165 / 0.18 / 0.195 us -> forward+Viterbi call
-//               8.52 / 8.49 / 8.29-8.69 / 8.41-8.56 ms, profiles/r3ab5_partition.txt)
-//   kFwdValu    a forward VALU half alone on its CU                            370 ns / column
-//   kBulkVit    Viterbi alone of a column in the per-wave launch               115 CU-ns / column
-//               (10 M columns of short blocks in 4.43 ms on 256 CUs)
-//   kVitWaveLatV  a per-wave Viterbi block's step in that launch under full    700 ns / column
-//               load (two waves per SIMD: ~640 ns alone), calibrated on the chr10 Viterbi-only
-//               call with 0 / 30 / 59 / 80 / 100 / 124 long blocks: 12.1 / 6.42 / 5.76 / 5.80 /
-//               6.02 / 7.97 ms (profiles/r4m_vit_long_set.txt; this rule picks 69)
-//   kMixFwd / kMixVit  the mixed queue's ordering weights: per-column step times under full
-//               load at N = 70 of a matrix-core forward group (~0.92 us) and a per-wave Viterbi
-//               block (~0.64 us), measured on chr10 (profiles/r3l_*)
-//   kMixPrio    mixed-queue entries that run at raised wave priority: about one per SIMD pair
-//   kVitPairEff the effective step of a 9-wave Viterbi block that shares its reserved CU with a
-//               second long block for part of its sweep (alone 318 ns, with a partner for the
-//               whole sweep 407 ns, three per CU 613 ns; profiles/r4pp_pair_long_blocks.txt);
-//   kPairShare  two long blocks per reserved CU only when the one-per-CU long set would hold
-//               more than this share of the chip: chr10 (35 CUs) 7.62-7.70 -> 7.44-7.48 ms
-//               per step with the long set on 24 CUs (same box, interleaved); the chr100
-//               shards (12-16 CUs) keep one per CU: paired with bins sized by 360 ns, one
-//               shard went 8.5 -> 9.5 ms (profiles/r4pab_pair_ab.txt)
-//   kPruneCol   a per-wave Viterbi block takes the bound-pruned step (fewer instructions per
-//               column, a longer dependent chain: wave_tasks.h) when its length x kPruneCol
-//               fits within the expected makespan, the full scan otherwise; chr10
-//               forward+Viterbi with 1.0 / 1.4 / 2.0 / 2.9 / 4.0 / 6.0 us and all blocks on the
-//               full scan: 7.95-7.99 / 7.64-7.65 / 7.67-7.73 / 7.82 / 7.85 / 7.94 / 8.12 ms per
-//               step; chr100 (every block pruned) 59.4 -> 51.6 ms, its world-8 shards 8.96 ->
-//               8.61 ms; the Viterbi-only call stays at its long set's floor (6.1 ms)
-//               (profiles/r4pc_prune_col.txt)
-//   kMixGroupCol  the per-column step a forward half may take in a matrix-core group and
-//               still finish within the expected makespan (sets the floor of the VALU-task
-//               threshold): chr100 world-8 shards with 0.7 / 1.0 / 1.4 us -> slowest shard
-//               14.05 / 12.17 / 10.31 ms vs 10.75 ms with the fraction rule alone
-//               (profiles/r4w_shard_threshold.txt)
-// Calibrated at N = 70 only; tests/test_partition.py pins the decisions they produce for the
-// benchmark layouts, so that a recalibration cannot move a layout onto another branch unseen.
-constexpr double kVitLone = 325e-9, kVitWaveLat = 800e-9, kBulkCu = 180e-9, kFwdValu = 370e-9,
-                 kBulkVit = 115e-9, kVitWaveLatV = 700e-9, kMixFwd = 0.92, kMixVit = 0.64,
-                 kMixGroupCol = 1.4e-6, kPruneCol = 1.4e-6, kVitPairEff = 360e-9,
-                 kPairShare = 1.0 / 8, kFwdPairStep = 480e-9;
-constexpr int kFwdPairMin = 16;
-constexpr int64_t kMixPrio = 512;
-
-// Bins of capacity `cap` (first fit, items longest first): the CUs a set of sequential tasks
-// needs to finish within cap
-int ffd_bins(const std::vector<int64_t>& items, double cap) {
-  std::vector<double> bins;
-  for (int64_t t : items) {
-    bool placed = false;
-    for (double& b : bins)
-      if (b + (double)t <= cap) {
-        b += (double)t;
-        placed = true;
-        break;
-      }
-    if (!placed) bins.push_back((double)t);
-  }
-  return (int)bins.size();
-}
-
-// The forward+Viterbi CU partition of a plan (viterbi_impl).  Expected makespan T: the whole
-// workload at the bulk layouts' throughput over every CU, or the longest block alone on the
-// 9-wave layout, whichever is longer.  A block whose per-wave Viterbi step latency would
-// exceed T joins the long set; the long set gets the CUs it needs to finish within T at the
-// lone-block step time, the forward's VALU halves (`ulen`) the CUs they need at theirs,
-// rounded up to whole XCC sets (8 CUs: one per XCC).  The reserved CUs join the bulk queue
-// when their long work is done, so a generous reservation costs little.
-void plan_partition(itr_plan_t p, const std::vector<int64_t>& ulen, int cus) {
-  const int64_t nblocks = p->nblocks;
-  const double tmax = nblocks ? (double)p->sorted_len[0] : 0.0;
-  double wlat = kVitWaveLat, bulk = kBulkCu;
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_WAVE_LAT")) wlat = atof(getenv("ITR_WAVE_LAT"));
-  if (getenv("ITR_BULK_CU")) bulk = atof(getenv("ITR_BULK_CU"));
-#endif
-  const double T = std::max((double)p->total * bulk / cus, tmax * kVitLone);
-  int64_t k = 0, cols = 0;
-  std::vector<int64_t> lng;
-  while (k < nblocks && p->sorted_len[k] >= 2048 && (double)p->sorted_len[k] * wlat > T) {
-    lng.push_back(p->sorted_len[k]);
-    cols += p->sorted_len[k++];
-  }
-  p->vit_nlong = k;
-  p->vit_long_cols = cols;
-  // Long blocks a reserved CU sweeps at a time: two (bins sized by the shared step
-  // kVitPairEff) when the one-per-CU long set would hold more than kPairShare of the chip
-  // and its longest block still fits the makespan at the shared step — the freed CUs go to
-  // the bulk; otherwise one.
-  double step = kVitLone, pstep = kVitPairEff;
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_VIT_PAIR")) pstep = atof(getenv("ITR_VIT_PAIR"));
-#endif
-  int lpc = 1;
-  if (ffd_bins(lng, T / kVitLone) > kPairShare * cus && tmax * pstep <= T) {
-    lpc = 2;
-    step = pstep;
-  }
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_LONG_PER_CU")) lpc = std::max(1, atoi(getenv("ITR_LONG_PER_CU")));
-#endif
-  p->long_per_cu = lpc;
-  const int rv = (ffd_bins(lng, T / step) + lpc - 1) / lpc;
-  std::vector<int64_t> halves(ulen);
-  std::sort(halves.begin(), halves.end(), std::greater<int64_t>());
-  int rf = ffd_bins(halves, T / kFwdValu);
-  // two forward halves per reserved CU at a time when the one-per-CU set is large (more
-  // than kFwdPairMin CUs), bins sized by the shared step kFwdPairStep
-  int fpc = 1;
-  const double fstep = kFwdPairStep;
-  const int fmin = kFwdPairMin;
-  if (rf > fmin) {
-    const int rf2 = (ffd_bins(halves, T / fstep) + 1) / 2;
-    if (rf2 < rf) {
-      rf = rf2;
-      fpc = 2;
-    }
-  }
-  p->fwd_per_cu = fpc;
-  p->fwd_reserve = rf;  // (viterbi_impl rounds both up to whole XCC sets)
-  p->vit_reserve = rv;
-  p->wave_ok = rv + rf <= cus / 2;
-  // the Viterbi-only call (itr_viterbi) on the same two reserved sets: its own makespan (the
-  // per-wave Viterbi's bulk cost, no forward) decides its long set, which both reserved sets
-  // sweep before they join the bulk
-  const double Tv = std::max((double)p->total * kBulkVit / cus, tmax * kVitLone);
-  int64_t kv = 0;
-  while (kv < nblocks && p->sorted_len[kv] >= 2048 && (double)p->sorted_len[kv] * kVitWaveLatV > Tv)
-    ++kv;
-  p->vit_nlong_v = kv;
-  // the per-wave Viterbi's step per block: bound-pruned below these lengths (kPruneCol)
-  double pcol = kPruneCol;
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_VIT_NLONG_V")) p->vit_nlong_v = atoi(getenv("ITR_VIT_NLONG_V"));
-  if (getenv("ITR_PRUNE_COL")) pcol = atof(getenv("ITR_PRUNE_COL"));
-#endif
-  p->vit_prune_len = (int)std::min(T / pcol, (double)INT32_MAX);
-  p->vit_prune_len_v = (int)std::min(Tv / pcol, (double)INT32_MAX);
-  if (getenv("ITR_VERBOSE"))
-    fprintf(stderr, "[itr] partition: T %.3f ms, long %lld blocks (%lld cols), rv %d rf %d (%zu halves)%s, "
-            "pruned below %d / %d columns\n",
-            T * 1e3, (long long)k, (long long)cols, p->vit_reserve, rf, halves.size(),
-            p->wave_ok ? "" : ", no wave layout", p->vit_prune_len, p->vit_prune_len_v);
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_VIT_RESERVE")) p->vit_reserve = atoi(getenv("ITR_VIT_RESERVE"));
-  if (getenv("ITR_FWD_RESERVE")) p->fwd_reserve = atoi(getenv("ITR_FWD_RESERVE"));
-#endif
-}
-
-// The posterior's concurrent split (launch_post_split): only on the VALU-only posterior
-// (no matrix-core form at this state count) and only where the blocks are few
-// (latency-bound: 10 Mbp in 100 blocks of 100 kbp, 96.9 -> 60 ms); with thousands of blocks
-// the sweeps are throughput-bound and the extra beta rows cost more than the shorter tail
-// (chr10: 20.7 vs 23.4 ms).  reserve() sizes the beta rows by the same test.
-// (the VALU-only concurrent split takes few-block workloads at N <= 128 even where the
 // matrix-core posterior exists: 100 blocks of 100 kbp at N = 70, 51.3 against 61.4 ms)
 bool post_split_path(int n, itr_plan_t p) {
   return p->npsplit > 0 && n <= 128 && p->nblocks <= 2 * (int64_t)cu_count();
+}
+
+// posterior (matrix-core form): blocks at least this fraction of the longest get their
+// backward sweep beside their forward one (itr_posterior)
+constexpr double kPostBetaFrac = 0.5;
+constexpr double kPostBetaLo = 0.4;  // their split column, as a fraction of their length
+
+// The matrix-core posterior's split set: the first nbeta blocks of the order (VALU tasks of
+// the backward launch, at least kPostBetaFrac of the longest block and >= 512 columns) and
+// their beta rows (brows = their columns).  itr_posterior splits them, reserve() sizes their
+// rows with it.
+std::pair<int64_t, int64_t> hybrid_beta_set(itr_plan_t p, int n) {
+  if (p->nblocks == 0) return {0, 0};
+  const itr::MfmaGeometry gb = itr::mfma_geometry(n, itr::MODE_BWD);
+  int64_t nurg = 0, nbeta = 0, brows = 0;
+  const double lim = std::max(512.0, gb.pfrac * (double)p->sorted_len[0]);
+  while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
+  const double blim = std::max(512.0, kPostBetaFrac * (double)p->sorted_len[0]);
+  while (nbeta < std::min(p->npsplit, nurg) && (double)p->sorted_len[nbeta] >= blim)
+    brows += p->sorted_len[nbeta++];
+  return {nbeta, brows};
 }
 
 int reserve(itr_plan_t p, int n, bool vit, bool post) {
@@ -568,10 +257,20 @@ int reserve(itr_plan_t p, int n, bool vit, bool post) {
     const int stride = g.cfg >= 0 ? std::max(xa, g.xr) : xa;
     need_rows = std::max(need_rows, (size_t)p->total * stride);
   }
-  if (post && post_split_path(n, p) && (size_t)p->beta_rows * xa > p->beta_cap) {
+  // beta rows: the VALU-only concurrent split's (stride xa) or the matrix-core posterior's
+  // split set (stride of its forward-store rows), whichever itr_posterior will take
+  size_t beta_need = 0;
+  if (post && post_split_path(n, p)) {
+    beta_need = (size_t)p->beta_rows * xa;
+  } else if (post) {
+    const itr::MfmaGeometry gf = itr::mfma_geometry(n, itr::MODE_FWD_STORE);
+    if (gf.cfg >= 0) beta_need = (size_t)hybrid_beta_set(p, n).second * gf.xr;
+  }
+  if (beta_need > p->beta_cap) {
     dev_free(p->d_beta);
-    if (int e = dev_alloc(&p->d_beta, (size_t)p->beta_rows * xa)) return e;
-    p->beta_cap = (size_t)p->beta_rows * xa;
+    p->beta_cap = 0;
+    if (int e = dev_alloc(&p->d_beta, beta_need)) return e;
+    p->beta_cap = beta_need;
   }
   if (need_rows > p->alpha_cap) {
     dev_free(p->d_alpha);
@@ -637,11 +336,7 @@ int run_sweep(int mode, itr::SweepArgs a, hipStream_t st, const char* tname,
 // valu / mfma: launch the VALU tasks / the matrix-core groups (both: one launch; one of them:
 // that part only, so the two can run on different CU sets); zero_queues: reset the two work
 // counters on `st` first (a split launch resets them once, before both parts).
-// posterior (matrix-core form): blocks at least this fraction of the longest get their
-// backward sweep beside their forward one (itr_posterior)
-constexpr double kPostBetaFrac = 0.5;
-constexpr double kPostBetaLo = 0.4;  // their split column, as a fraction of their length
-constexpr int64_t kCombCols = 256;     // columns per combine task of the backward launch
+constexpr int64_t kCombCols = 256;  // columns per combine task of the posterior's backward launch
 
 // nbeta (posterior, forward-store launch): the first nbeta blocks of the order also get a
 // backward task storing beta rows into v.beta (over [v.sub_lo[block], T)).
@@ -695,9 +390,6 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   }
   const int64_t work = v.nblocks + v.nbeta + (a.ngroups + g.gb - 1) / g.gb;
   int per_cu = g.per_cu;
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_HYB_PER_CU")) per_cu = atoi(getenv("ITR_HYB_PER_CU"));
-#endif
   int64_t grid = std::min<int64_t>((int64_t)per_cu * cus, work);
   if (max_grid > 0) grid = std::min(grid, max_grid);
   if (grid <= 0) return 0;
@@ -796,11 +488,7 @@ int itr_model_create(int n, const double* a, const double* la, const double* E,
     m->h_PIE.assign(PIE, PIE + (size_t)256 * n);
   }
   const itr::WaveMfmaGeometry wf = itr::wave_mfma_geometry(n);
-#ifdef ITR_EXPERIMENT
-  const bool need_ef = wf.cfg >= 0;  // ITR_WAVE_FWD: the per-wave forward at every size
-#else
-  const bool need_ef = wf.mixed;     // the mixed launch's forward groups
-#endif
+  const bool need_ef = wf.mixed;  // the mixed launch's forward groups
   if (need_ef) {
     const int w = wf.er;
     std::vector<double> ef((size_t)(ITR_NOBS + 1) * w, 0.0);
@@ -846,377 +534,6 @@ int itr_model_n_states(itr_model_t m, int* n) {
   return 0;
 }
 
-int itr_plan_create(const int64_t* off, int64_t nblocks, itr_plan_t* out) {
-  return itr_plan_create_ex(off, nblocks, -1.0, -1.0, out);
-}
-
-namespace {
-// cus > 0: plan for that many CUs instead of the device's; host_only: the host-side plan
-// (task lists, CU partition) without device allocations or uploads (itr_plan_partition_info)
-int plan_create_impl(const int64_t* off, int64_t nblocks, double split_frac,
-                     double post_split_frac, int cus, bool host_only, itr_plan_t* out) {
-  if (!out) return fail(ITR_EINVAL, "null output pointer");
-  *out = nullptr;
-  if (nblocks < 0 || (nblocks > 0 && !off)) return fail(ITR_EINVAL, "bad block offsets");
-  if (nblocks > INT32_MAX) return fail(ITR_EINVAL, "too many blocks");
-  std::vector<int64_t> h_off(off, off + nblocks + 1);
-  if (h_off[0] != 0) return fail(ITR_EINVAL, "block_off[0] must be 0");
-  for (int64_t k = 0; k < nblocks; ++k) {
-    if (h_off[k + 1] < h_off[k]) return fail(ITR_EINVAL, "block offsets decrease at %lld",
-                                            (long long)k);
-    if (h_off[k + 1] - h_off[k] > INT32_MAX) return fail(ITR_EINVAL, "block too long");
-  }
-  auto* p = new itr_plan();
-  (void)hipGetDevice(&p->device);
-  p->nblocks = nblocks;
-  p->total = h_off[nblocks];
-  p->h_off = h_off;
-  std::vector<int64_t> tile_off(nblocks + 1, 0);
-  for (int64_t k = 0; k < nblocks; ++k)
-    tile_off[k + 1] = tile_off[k] + itr::vit_tiles(h_off[k + 1] - h_off[k]);
-  p->ntiles = tile_off[nblocks];
-  // longest-first processing order (stable: equal lengths keep block order)
-  std::vector<int32_t> order(nblocks);
-  std::iota(order.begin(), order.end(), 0);
-  std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) {
-    return h_off[x + 1] - h_off[x] > h_off[y + 1] - h_off[y];
-  });
-  p->sorted_len.resize(nblocks);
-  for (int64_t k = 0; k < nblocks; ++k) p->sorted_len[k] = h_off[order[k] + 1] - h_off[order[k]];
-  p->h_order.assign(order.begin(), order.end());
-  if (nblocks > 0) {
-    const int64_t k = std::min<int64_t>(nblocks - 1, 255);
-    const int64_t T = h_off[order[k] + 1] - h_off[order[k]];
-    p->prio_len = (int)std::max<int64_t>(T, 1);
-  }
-  // Forward log-likelihood tasks.  The longest block bounds the sweep's makespan (one
-  // workgroup steps it column by column), so blocks at least half as long as the longest
-  // (and >= 512 columns) become two half-length tasks — forward over the first half,
-  // textbook backward over the second — whose vectors fwd_split_combine_kernel joins.
-  // Tasks run longest first.  Two task lists over the same split blocks (slots):
-  //   tasks   every block (the VALU-only sweep, state counts without a matrix-core form);
-  //   the hybrid sweeps' own lists below.
-  const int64_t tmax = nblocks ? h_off[order[0] + 1] - h_off[order[0]] : 0;
-  std::vector<int32_t> split_blk;
-  // split_frac (itr_plan_create_ex; negative = the default 0.5): 0 disables the split (tests
-  // compare the split forward with the unsplit one)
-  const double frac = split_frac < 0 ? 0.5 : split_frac;
-  auto is_split = [&](int64_t T) {
-    return frac > 0 && T >= 512 && (double)T >= frac * (double)tmax;
-  };
-  std::vector<int32_t> slot_of(nblocks, -1);
-  for (int64_t k = 0; k < nblocks; ++k) {
-    const int32_t b = order[k];
-    if (is_split(h_off[b + 1] - h_off[b])) {
-      slot_of[b] = (int32_t)split_blk.size();
-      split_blk.push_back(b);
-    }
-  }
-  // posterior split set (blocks at least post_split_frac of the longest, default a quarter,
-  // >= 512 columns; 0 disables): a prefix of the order
-  std::vector<int64_t> boff(nblocks, -1);
-  {
-    const double pfrac = post_split_frac < 0 ? 0.25 : post_split_frac;
-    int64_t rows = 0, k = 0;
-    for (; k < nblocks; ++k) {
-      const int64_t T = h_off[order[k] + 1] - h_off[order[k]];
-      if (!(pfrac > 0 && T >= 512 && (double)T >= pfrac * (double)tmax)) break;
-      boff[order[k]] = rows;
-      rows += T;
-    }
-    p->npsplit = k;
-    p->beta_rows = rows;
-  }
-  auto make_tasks = [&](int64_t count) {
-    std::vector<int32_t> tasks;
-    std::vector<int64_t> tlen;
-    for (int64_t k = 0; k < count; ++k) {
-      const int32_t b = order[k];
-      const int64_t T = h_off[b + 1] - h_off[b];
-      if (slot_of[b] >= 0) {
-        const int32_t m = (int32_t)(T / 2), slot = slot_of[b];
-        tasks.insert(tasks.end(), {b, m, slot, b, -m, slot});
-        tlen.push_back(m);
-        tlen.push_back(T - m + 1);
-      } else {
-        tasks.insert(tasks.end(), {b, 0, 0});
-        tlen.push_back(T);
-      }
-    }
-    std::vector<int64_t> idx(tlen.size());
-    std::iota(idx.begin(), idx.end(), 0);
-    std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return tlen[x] > tlen[y]; });
-    std::vector<int32_t> sorted(tasks.size());
-    for (size_t k = 0; k < idx.size(); ++k)
-      for (int c = 0; c < 3; ++c) sorted[3 * k + c] = tasks[3 * idx[k] + c];
-    return sorted;
-  };
-  std::vector<int32_t> tasks = make_tasks(nblocks);
-  // groups of four `tasks` ids for the per-wave matrix-core forward on its own
-  // (ITR_WAVE_FWD, experiment library only): forward-shaped tasks and backward halves apart (a
-  // group shares its matrix operand), each kind longest first (the task list is sorted
-  // longest first)
-  std::vector<int32_t> wgroups;
-#ifdef ITR_EXPERIMENT
-  {
-    std::vector<int32_t> fw, bw;
-    for (int64_t k = 0; k < (int64_t)tasks.size() / 3; ++k)
-      (tasks[3 * k + 1] < 0 ? bw : fw).push_back((int32_t)k);
-    auto tlen = [&](int32_t k) {
-      const int32_t b = tasks[3 * k], sp = tasks[3 * k + 1];
-      const int64_t Tb = h_off[b + 1] - h_off[b];
-      return sp > 0 ? (int64_t)sp : (sp < 0 ? Tb + sp + 1 : Tb);
-    };
-    size_t fi = 0, bi = 0;
-    while (fi < fw.size() || bi < bw.size()) {
-      const bool pick_f = bi >= bw.size() || (fi < fw.size() && tlen(fw[fi]) >= tlen(bw[bi]));
-      auto& v = pick_f ? fw : bw;
-      size_t& i = pick_f ? fi : bi;
-      for (int r = 0; r < 4; ++r) wgroups.push_back(i < v.size() ? v[i++] : -1);
-    }
-  }
-#endif
-  // Hybrid sweeps (mfma_sweeps.hip).  A matrix-core group steps four blocks in about twice
-  // the VALU step time, so the longest work stays on the lower-latency VALU path and the
-  // bulk goes through the matrix cores.  Forward log-likelihood, with
-  // L = ufrac * longest:  T > 2L -> VALU tasks (split halves as above);  L < T <= 2L -> two
-  // matrix-core halves (first half forward, second half the textbook backward);  T <= L ->
-  // whole block in a matrix-core group.  (The posterior's split is chosen per call, run_hybrid.)
-  // Split slots of the hybrid forward are numbered separately (hsplit_blk).
-  // ufrac measured on the (5,5) model, 10 Mbp (scripts/gpu_r2b.sh: 0.12 / 0.18 / 0.22 / 0.25
-  // / 0.28 / 0.33 -> forward 4.93 / 4.24 / 3.97 / 3.85 / 3.80 / 3.97 ms)
-  double ufrac = 0.28;
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_URGENT_FRAC")) ufrac = atof(getenv("ITR_URGENT_FRAC"));
-#endif
-  // ... and never below what a matrix-core group finishes within the plan's expected makespan
-  // (kMixGroupCol per column of its longest member): a smaller alignment with a short longest
-  // block (a chr100 shard) would otherwise send many blocks to the VALU tasks and reserve CUs
-  // for them that the bulk needs
-  double colns = kMixGroupCol;
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_URGENT_COLNS")) colns = atof(getenv("ITR_URGENT_COLNS")) * 1e-9;
-#endif
-  double L = std::max(256.0, ufrac * (double)tmax);
-  if (colns > 0) {
-    const int ncu = cus > 0 ? cus : cu_count();
-    const double Tm = std::max((double)h_off[nblocks] * kBulkCu / ncu, (double)tmax * kVitLone);
-    L = std::max(L, Tm / colns);
-  }
-  std::vector<int32_t> hsplit_blk, utasks, mtasks;
-  std::vector<int64_t> ulen;
-  struct MT { int32_t id; int64_t steps; bool bwd; };
-  std::vector<MT> fwd_t, bwd_t;
-  for (int64_t k = 0; k < nblocks; ++k) {
-    const int32_t b = order[k];
-    const int64_t T = h_off[b + 1] - h_off[b];
-    if ((double)T > 2 * L) {
-      if (is_split(T)) {
-        const int32_t m = (int32_t)(T / 2), slot = (int32_t)hsplit_blk.size();
-        hsplit_blk.push_back(b);
-        utasks.insert(utasks.end(), {b, m, slot, b, -m, slot});
-        ulen.push_back(m);
-        ulen.push_back(T - m + 1);
-      } else {
-        utasks.insert(utasks.end(), {b, 0, 0});
-        ulen.push_back(T);
-      }
-    } else if ((double)T > L && T >= 512) {
-      const int32_t m = (int32_t)(T / 2), slot = (int32_t)hsplit_blk.size();
-      hsplit_blk.push_back(b);
-      fwd_t.push_back({(int32_t)(mtasks.size() / 3), m, false});
-      mtasks.insert(mtasks.end(), {b, m, slot});
-      bwd_t.push_back({(int32_t)(mtasks.size() / 3), T - m + 1, true});
-      mtasks.insert(mtasks.end(), {b, -m, slot});
-    } else {
-      fwd_t.push_back({(int32_t)(mtasks.size() / 3), T, false});
-      mtasks.insert(mtasks.end(), {b, 0, 0});
-    }
-  }
-  {  // VALU tasks longest first
-    std::vector<int64_t> idx(ulen.size());
-    std::iota(idx.begin(), idx.end(), 0);
-    std::stable_sort(idx.begin(), idx.end(), [&](int64_t x, int64_t y) { return ulen[x] > ulen[y]; });
-    std::vector<int32_t> sorted(utasks.size());
-    for (size_t k = 0; k < idx.size(); ++k)
-      for (int c = 0; c < 3; ++c) sorted[3 * k + c] = utasks[3 * idx[k] + c];
-    utasks.swap(sorted);
-  }
-  // matrix-core groups: forward-shaped tasks and second halves grouped separately (a group
-  // shares its matrix operand), longest first, merged two groups at a time so that a
-  // workgroup running two groups (GB = 2) always gets two of one kind
-  auto by_steps = [](const MT& x, const MT& y) { return x.steps > y.steps; };
-  std::stable_sort(fwd_t.begin(), fwd_t.end(), by_steps);
-  std::stable_sort(bwd_t.begin(), bwd_t.end(), by_steps);
-  std::vector<int32_t> groups_ll;
-  {
-    size_t fi = 0, bi2 = 0;
-    auto take_group = [&](std::vector<MT>& v, size_t& i) {
-      for (int r = 0; r < 4; ++r) groups_ll.push_back(i < v.size() ? v[i++].id : -1);
-    };
-    while (fi < fwd_t.size() || bi2 < bwd_t.size()) {
-      const bool pick_f = bi2 >= bwd_t.size() ||
-                          (fi < fwd_t.size() && fwd_t[fi].steps >= bwd_t[bi2].steps);
-      for (int g = 0; g < 2; ++g) {
-        if (pick_f) take_group(fwd_t, fi);
-        else take_group(bwd_t, bi2);
-      }
-    }
-  }
-  // Viterbi long set and the CU partition of the forward+Viterbi call
-  plan_partition(p, ulen, cus > 0 ? cus : cu_count());
-  // The mixed queue: forward groups (steps = their longest member) and the remaining Viterbi
-  // blocks merged by expected duration (kMixFwd, kMixVit), longest first.
-  std::vector<int32_t> mix;
-  {
-    const int64_t ng = (int64_t)groups_ll.size() / 4;
-    std::vector<int64_t> gsteps(ng, 0);
-    for (int64_t g = 0; g < ng; ++g)
-      for (int r = 0; r < 4; ++r) {
-        const int32_t id = groups_ll[4 * g + r];
-        if (id < 0) continue;
-        const int32_t b = mtasks[3 * id], sp = mtasks[3 * id + 1];
-        const int64_t Tb = h_off[b + 1] - h_off[b];
-        gsteps[g] = std::max(gsteps[g], sp > 0 ? (int64_t)sp : (sp < 0 ? Tb + sp + 1 : Tb));
-      }
-    std::vector<int64_t> gidx(ng);
-    std::iota(gidx.begin(), gidx.end(), 0);
-    std::stable_sort(gidx.begin(), gidx.end(), [&](int64_t x, int64_t y) { return gsteps[x] > gsteps[y]; });
-    const double cf = kMixFwd, cv = kMixVit;
-    int64_t gi = 0, vi = p->vit_nlong;
-    const int64_t nprio = kMixPrio;
-    while (gi < ng || vi < nblocks) {
-      const bool take_f = vi >= nblocks ||
-                          (gi < ng && cf * (double)gsteps[gidx[gi]] >= cv * (double)p->sorted_len[vi]);
-      if ((int64_t)mix.size() == nprio) {
-        p->mix_prio_fwd = (int)std::max<int64_t>(1, gi < ng ? gsteps[gidx[gi]] : 1);
-        p->mix_prio_vit = (int)std::max<int64_t>(1, vi < nblocks ? p->sorted_len[vi] : 1);
-      }
-      if (take_f) mix.push_back(-(int32_t)gidx[gi++] - 1);
-      else mix.push_back(order[vi++]);
-    }
-    p->nmix = (int64_t)mix.size();
-  }
-  p->nwgroups = (int64_t)wgroups.size() / 4;
-  p->nutasks = (int64_t)utasks.size() / 3;
-  p->ngroups_ll = (int64_t)groups_ll.size() / 4;
-  p->nhsplit = (int64_t)hsplit_blk.size();
-  p->ntasks = (int64_t)tasks.size() / 3;
-  p->nsplit = (int64_t)split_blk.size();
-  if (host_only) {
-    *out = p;
-    return 0;
-  }
-  int e = 0;
-  if (!e) e = dev_alloc(&p->d_tasks, tasks.size());
-  if (!e) e = dev_alloc(&p->d_wgroups, wgroups.size());
-  if (!e) e = dev_alloc(&p->d_mix, mix.size());
-  if (!e) e = dev_alloc(&p->d_utasks, utasks.size());
-  if (!e) e = dev_alloc(&p->d_mtasks, mtasks.size());
-  if (!e) e = dev_alloc(&p->d_groups_ll, groups_ll.size());
-  if (!e) e = dev_alloc(&p->d_hsplit_blk, hsplit_blk.size());
-  if (!e) e = dev_alloc(&p->d_split_blk, split_blk.size());
-  const size_t nslots = (size_t)std::max(p->nsplit, p->nhsplit);
-  if (!e) e = dev_alloc(&p->d_svec, nslots * 2 * 256);
-  if (!e) e = dev_alloc(&p->d_sK, nslots * 2);
-  if (!e) e = dev_alloc(&p->d_off, nblocks + 1);
-  if (!e) e = dev_alloc(&p->d_tile_off, nblocks + 1);
-  if (!e) e = dev_alloc(&p->d_boff, nblocks);
-  if (!e) e = dev_alloc(&p->d_order, nblocks);
-  if (!e) e = dev_alloc(&p->d_queue, 16);
-  if (!e && hipMemset(p->d_queue, 0, 16 * sizeof(int)) != hipSuccess)
-    e = fail(ITR_EHIP, "plan workspace init failed");
-  if (!e) e = dev_alloc(&p->d_sink, 64 * (size_t)itr::kSinkWgs);
-  if (!e) e = dev_alloc(&p->d_last, nblocks);
-  auto up = [&](void* d, const void* h, size_t bytes) {
-    if (e || bytes == 0) return;
-    if (hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) != hipSuccess)
-      e = fail(ITR_EHIP, "plan upload failed");
-  };
-  up(p->d_off, h_off.data(), (nblocks + 1) * sizeof(int64_t));
-  up(p->d_tile_off, tile_off.data(), (nblocks + 1) * sizeof(int64_t));
-  up(p->d_boff, boff.data(), nblocks * sizeof(int64_t));
-  up(p->d_order, order.data(), nblocks * sizeof(int32_t));
-  up(p->d_tasks, tasks.data(), tasks.size() * sizeof(int32_t));
-  up(p->d_wgroups, wgroups.data(), wgroups.size() * sizeof(int32_t));
-  up(p->d_mix, mix.data(), mix.size() * sizeof(int32_t));
-  up(p->d_utasks, utasks.data(), utasks.size() * sizeof(int32_t));
-  up(p->d_mtasks, mtasks.data(), mtasks.size() * sizeof(int32_t));
-  up(p->d_groups_ll, groups_ll.data(), groups_ll.size() * sizeof(int32_t));
-  up(p->d_hsplit_blk, hsplit_blk.data(), hsplit_blk.size() * sizeof(int32_t));
-  up(p->d_split_blk, split_blk.data(), split_blk.size() * sizeof(int32_t));
-  if (e) {
-    itr_plan_destroy(p);
-    return e;
-  }
-  *out = p;
-  return 0;
-}
-}  // namespace
-
-int itr_plan_create_ex(const int64_t* off, int64_t nblocks, double split_frac,
-                       double post_split_frac, itr_plan_t* out) {
-  return plan_create_impl(off, nblocks, split_frac, post_split_frac, 0, false, out);
-}
-
-int itr_plan_partition_info(const int64_t* off, int64_t nblocks, int cus, int64_t* out) {
-  if (!out || cus < 1) return fail(ITR_EINVAL, "bad arguments");
-  itr_plan_t p = nullptr;
-  if (int e = plan_create_impl(off, nblocks, -1.0, -1.0, cus, true, &p)) return e;
-  out[0] = p->vit_nlong;
-  out[1] = p->vit_long_cols;
-  out[2] = p->vit_reserve;
-  out[3] = p->fwd_reserve;
-  out[4] = p->wave_ok ? 1 : 0;
-  out[5] = p->vit_nlong_v;
-  out[6] = p->nutasks;
-  out[7] = p->nmix;
-  out[8] = p->vit_prune_len;
-  out[9] = p->vit_prune_len_v;
-  delete p;  // (host-only: nothing on the device)
-  return 0;
-}
-
-int itr_plan_set_prune_len(itr_plan_t p, int64_t len) {
-  if (int e = check_plan(p)) return e;
-  p->prune_override = len < 0 ? -1 : len;
-  return 0;
-}
-
-int itr_plan_destroy(itr_plan_t p) {
-  if (!p) return 0;
-  dev_free(p->d_off);
-  dev_free(p->d_tile_off);
-  dev_free(p->d_boff);
-  dev_free(p->d_sublo);
-  dev_free(p->d_comb);
-  dev_free(p->d_beta);
-  dev_free(p->d_order);
-  dev_free(p->d_queue);
-  dev_free(p->d_sink);
-  dev_free(p->d_stay);
-  dev_free(p->d_tasks);
-  dev_free(p->d_wgroups);
-  dev_free(p->d_mix);
-  dev_free(p->d_utasks);
-  dev_free(p->d_mtasks);
-  dev_free(p->d_groups_ll);
-  dev_free(p->d_hsplit_blk);
-  dev_free(p->d_split_blk);
-  dev_free(p->d_svec);
-  dev_free(p->d_sK);
-  dev_free(p->d_last);
-  dev_free(p->d_alpha);
-  delete p;
-  return 0;
-}
-
-int itr_plan_total_columns(itr_plan_t p, int64_t* total) {
-  if (!p || !total) return fail(ITR_EINVAL, "null pointer");
-  *total = p->total;
-  return 0;
-}
-
 int itr_plan_reserve(itr_plan_t p, int n, int for_posterior) {
   if (int e = check_plan(p)) return e;
   if (n < 1 || n > ITR_MAX_STATES) return fail(ITR_EINVAL, "bad n_states");
@@ -1253,38 +570,6 @@ int forward_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* logli
     return fail(ITR_ESTATE, "forward task tables missing");
   const itr::MfmaGeometry g = itr::mfma_geometry(m->n, itr::MODE_FWD_LL);
   int xr = itr::sweep_row_stride(m->n, itr::MODE_FWD_LL);
-#ifdef ITR_EXPERIMENT
-  const itr::WaveMfmaGeometry wf = itr::wave_mfma_geometry(m->n);
-  if (getenv("ITR_WAVE_FWD") && wf.cfg >= 0 && m->EF && p->nwgroups > 0) {
-    itr::WaveMfmaArgs w{};
-    w.n = m->n;
-    w.ngroups = p->nwgroups;
-    w.groups = p->d_wgroups;
-    w.tasks = p->d_tasks;
-    w.queue = p->d_queue + 11;
-    w.off = p->d_off;
-    w.obs = obs;
-    w.a = m->a;
-    w.aT = m->aT;
-    w.ef = m->EF;
-    w.emit = m->E;
-    w.init = m->PIE;
-    w.loglik = loglik;
-    w.svec = p->d_svec;
-    w.sstride = wf.er;
-    w.sK = p->d_sK;
-    w.prio_len = INT32_MAX;
-    const int64_t grid = std::min<int64_t>((int64_t)wf.per_cu * cu_count(), (p->nwgroups + 3) / 4);
-    HIP_TRY(hipMemsetAsync(w.queue, 0, sizeof(int), st));
-    {
-      Scope sc("forward", st);
-      HIP_TRY(itr::launch_wave_mfma(wf, (int)grid, w, st));
-    }
-    HIP_TRY(itr::launch_fwd_split_combine(m->n, wf.er, (int)p->nsplit, p->d_split_blk, p->d_svec,
-                                          p->d_sK, loglik, st));
-    return 0;
-  }
-#endif
   if (g.cfg >= 0 && p->ngroups_ll > 0) {
     a.tasks = p->d_utasks;
     a.nblocks = p->nutasks;
@@ -1375,9 +660,6 @@ int vit_slot_tables(itr_model_t m) {
   for (int b = 0; b < kSeq; ++b)
     for (int j = 0; j < n; ++j) fails[j] += fails_b[b][j];
   std::stable_sort(rank.begin(), rank.end(), [&](int x, int y) { return fails[x] > fails[y]; });
-#ifdef ITR_EXPERIMENT
-  if (getenv("ITR_VSLOT_NATURAL")) std::iota(rank.begin(), rank.end(), 0);
-#endif
   // rank k < 64: column k / 8 of group k % 8 (A slots); then the groups' B slots (column 8)
   const int iq = w / 8;
   std::vector<int32_t> slot(w, -1);
@@ -1530,9 +812,6 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     w.prune_len = p->prune_override >= 0
                       ? (int)std::min<int64_t>(p->prune_override, INT32_MAX)
                       : (vonly ? p->vit_prune_len_v : p->vit_prune_len);
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_PRUNE_LEN")) w.prune_len = atoi(getenv("ITR_PRUNE_LEN"));
-#endif
     w.log_e = m->LE;  // each bulk block traced by its wave right after its sweep
     w.path = path;
     trace_end = nlong;
@@ -1553,9 +832,6 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     const bool split_fwd = hyb_fwd && p->nutasks > 0 && p->fwd_reserve > 0;
     // (the mixed launch also serves a forward without VALU tasks: every half in the groups)
     bool mixed = hyb_fwd && (split_fwd || p->nutasks == 0) && wf.mixed && m->EF && p->nmix > 0;
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_NO_MIXED")) mixed = false;
-#endif
     itr::SweepArgs af = base_args(m, p, obs);
     af.mat = m->a;
     af.matT = m->aT;
@@ -1572,10 +848,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     // queue is shared with the reserved CUs' late launches)
     HIP_TRY(hipMemsetAsync(p->d_queue + 2, 0, 12 * sizeof(int), st));
     hipStream_t sb = st;
-    int ocus = cus - reserve_cus;  // CUs of the sb launches
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_MIX_CUS")) ocus = atoi(getenv("ITR_MIX_CUS"));
-#endif
+    const int ocus = cus - reserve_cus;  // CUs of the sb launches
     // the mixed launch: forward groups (the hybrid plan's matrix-core tasks) and the per-wave
     // Viterbi blocks from one queue ordered by expected duration (plan: mix list)
     itr::WaveMfmaArgs f{};
@@ -1642,10 +915,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
             return e;
       }
       if (split_fwd) {
-        int64_t fg = (int64_t)p->fwd_per_cu * rfr;  // forward halves at a time on the set
-#ifdef ITR_EXPERIMENT
-        if (getenv("ITR_FWD_PER_CU")) fg = (int64_t)atoi(getenv("ITR_FWD_PER_CU")) * rfr;
-#endif
+        const int64_t fg = (int64_t)p->fwd_per_cu * rfr;  // forward halves at a time on the set
         if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, pt->lng2, nullptr, true, false,
                                fg, false, 0, fg > rfr))
           return e;
@@ -1698,12 +968,10 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     // 15 % on the config-2 layout (71 vs 25 ms) and 46 % deep inside long blocks (3.2 us per
     // lone column vs 0.64 on the 9-wave layout); at N = 95 the 9-wave layout wins throughout.
     const int64_t mean_len = p->total / std::max<int64_t>(1, p->nblocks);
-    bool prune = pg.waves > 0 && m->MJ && m->n > 128 && mean_len <= 400 &&
+    // (at least four blocks per CU: N = 137..140 fit one or two beside the matrix, far below
+    // the measured regime; N = 141..144 do not fit at all, pg.waves = 0)
+    bool prune = pg.waves >= 4 && m->MJ && m->n > 128 && mean_len <= 400 &&
                  p->nblocks > 2 * cus;
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_NO_PRUNE_VIT")) prune = false;
-    if (getenv("ITR_PV_FORCE")) prune = pg.waves > 0 && m->MJ;
-#endif
     if (prune) {
       // one block per wavefront, log a in LDS, the bound-pruned step (prune_vit.hip)
       itr::PruneVitArgs v{};
@@ -1729,24 +997,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       const int64_t grid = std::min<int64_t>(cus, (p->nblocks + pg.waves - 1) / pg.waves);
       std::optional<Scope> sc;
       if (!fwd_loglik) sc.emplace("viterbi", st);
-#ifdef ITR_EXPERIMENT
-      static unsigned long long* d_pvdiag = nullptr;
-      if (getenv("ITR_PV_DIAG")) {
-        if (!d_pvdiag) HIP_TRY(hipMalloc(&d_pvdiag, 4 * sizeof(unsigned long long)));
-        HIP_TRY(hipMemsetAsync(d_pvdiag, 0, 4 * sizeof(unsigned long long), st));
-        v.diag = d_pvdiag;
-      }
-#endif
       HIP_TRY(itr::launch_prune_vit(pg, (int)grid, v, st));
-#ifdef ITR_EXPERIMENT
-      if (v.diag) {
-        unsigned long long h[3];
-        HIP_TRY(hipMemcpyAsync(h, d_pvdiag, sizeof h, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        fprintf(stderr, "prune_vit: %llu steps, %.2f failing targets and %.2f passes per step\n",
-                h[0], (double)h[1] / std::max(1ull, h[0]), (double)h[2] / std::max(1ull, h[0]));
-      }
-#endif
     } else {
       if (int e = run_sweep(itr::MODE_VIT, a, st, "viterbi")) return e;
     }
@@ -1848,17 +1099,10 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
     // matrix-core bulk of the backward launch.  (Splitting the forward sweep as well — a
     // forward + posterior sweep over [hi, T) in the backward launch — measured slower: 24.1
     // against 23.0 ms per (7,7) posterior, profiles/r5ps3_*.)
-    const double bfrac = kPostBetaFrac, lofrac = kPostBetaLo;
+    const double lofrac = kPostBetaLo;
     // (split blocks are VALU tasks of the backward launch: a prefix of its VALU set, whose
     // limit mirrors run_hybrid's; their forward sweep is a VALU task or a matrix-core group)
-    int64_t nurg = 0, nbeta = 0, brows = 0;
-    {
-      const double lim = std::max(512.0, gb.pfrac * (double)p->sorted_len[0]);
-      while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
-    }
-    const double blim = std::max(512.0, bfrac * (double)p->sorted_len[0]);
-    while (nbeta < std::min(p->npsplit, nurg) && (double)p->sorted_len[nbeta] >= blim)
-      brows += p->sorted_len[nbeta++];
+    const auto [nbeta, brows] = hybrid_beta_set(p, m->n);
     if (nbeta > 0 && p->sublo_key != std::make_pair(nbeta, lofrac)) {
       if (!p->d_sublo)
         if (int e = dev_alloc(&p->d_sublo, p->nblocks)) return e;
@@ -1947,187 +1191,8 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
 }
 
 // ---- host conveniences -----------------------------------------------------------------
-namespace {
-struct DevBuf {
-  void* p = nullptr;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
-};
-
-// Device -> pageable host copy of a large result (the posterior rows: 10.6 GB per 10 Mbp at
-// N = 133).  A plain hipMemcpy stages through the runtime's pinned buffers and writes (and
-// page-faults) the destination from one thread; here chunks go to two pinned staging buffers
-// on their own stream while host threads copy the previous chunk out, so the PCIe transfer
-// overlaps the faulting copies and those run on several cores.
-constexpr size_t kStageBytes = size_t(128) << 20;
-// The calling thread's staging buffers, stream and events; they belong to one device and
-// are recreated when the thread's current device changes.  itr_release_staging() frees them.
-struct Staging {
-  int device = -1;
-  void* stage[2] = {nullptr, nullptr};
-  hipStream_t cs = nullptr;
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  void release() {
-    for (int i = 0; i < 2; ++i) {
-      if (stage[i]) (void)hipHostFree(stage[i]);
-      if (ev[i]) (void)hipEventDestroy(ev[i]);
-      stage[i] = nullptr;
-      ev[i] = nullptr;
-    }
-    if (cs) (void)hipStreamDestroy(cs);
-    cs = nullptr;
-    device = -1;
-  }
-};
-thread_local Staging g_stage;
-
-// The calling thread's pinned host buffer and device buffer of the host-block entry points
-// (grow-only, per device): no allocation, no pageable copy per call.
-struct HostIO {
-  int device = -1;
-  void* pin = nullptr;
-  size_t pin_cap = 0;
-  void* dbuf = nullptr;
-  size_t dcap = 0;
-  hipStream_t st = nullptr;  // the calls' own non-blocking stream (no legacy-stream syncs)
-  void release() {
-    if (st) (void)hipStreamSynchronize(st);
-    if (pin) (void)hipHostFree(pin);
-    if (dbuf) (void)hipFree(dbuf);
-    if (st) (void)hipStreamDestroy(st);
-    pin = dbuf = nullptr;
-    st = nullptr;
-    pin_cap = dcap = 0;
-    device = -1;
-  }
-  int reserve(size_t pin_bytes, size_t dev_bytes) {
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    if (dev != device) {
-      release();
-      device = dev;
-    }
-    if (!st) HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    if (pin_bytes > pin_cap) {
-      if (pin) (void)hipHostFree(pin);
-      pin = nullptr;
-      pin_cap = 0;
-      HIP_TRY(hipHostMalloc(&pin, pin_bytes, hipHostMallocDefault));
-      pin_cap = pin_bytes;
-    }
-    if (dev_bytes > dcap) {
-      if (dbuf) (void)hipFree(dbuf);
-      dbuf = nullptr;
-      dcap = 0;
-      HIP_TRY(hipMalloc(&dbuf, dev_bytes));
-      dcap = dev_bytes;
-    }
-    return 0;
-  }
-};
-thread_local HostIO g_hio;
-
-int copy_out_large(void* dst, const void* src, size_t bytes) {
-  if (bytes < 2 * kStageBytes) {
-    HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
-    return 0;
-  }
-  int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  Staging& sg = g_stage;
-  if (sg.device != dev) {
-    sg.release();
-    HIP_TRY(hipStreamCreateWithFlags(&sg.cs, hipStreamNonBlocking));
-    for (int i = 0; i < 2; ++i) {
-      HIP_TRY(hipHostMalloc(&sg.stage[i], kStageBytes, hipHostMallocDefault));
-      HIP_TRY(hipEventCreateWithFlags(&sg.ev[i], hipEventDisableTiming));
-    }
-    sg.device = dev;
-  }
-  void* const* stage = sg.stage;
-  hipStream_t cs = sg.cs;
-  hipEvent_t* ev = sg.ev;
-  HIP_TRY(hipStreamSynchronize(nullptr));  // the sweep ran on the null stream
-  const size_t nch = (bytes + kStageBytes - 1) / kStageBytes;
-  auto issue = [&](size_t c) -> int {
-    const size_t off = c * kStageBytes, len = std::min(kStageBytes, bytes - off);
-    HIP_TRY(hipMemcpyAsync(stage[c & 1], (const char*)src + off, len, hipMemcpyDeviceToHost,
-                           cs));
-    HIP_TRY(hipEventRecord(ev[c & 1], cs));
-    return 0;
-  };
-  if (int e = issue(0)) return e;
-  const int nt = 8;
-  for (size_t c = 0; c < nch; ++c) {
-    HIP_TRY(hipEventSynchronize(ev[c & 1]));
-    if (c + 1 < nch)
-      if (int e = issue(c + 1)) return e;
-    const size_t off = c * kStageBytes, len = std::min(kStageBytes, bytes - off);
-    const char* s = (const char*)stage[c & 1];
-    char* d = (char*)dst + off;
-    std::vector<std::thread> th;
-    for (int w = 1; w < nt; ++w)
-      th.emplace_back([=] { memcpy(d + len * w / nt, s + len * w / nt,
-                                   len * (w + 1) / nt - len * w / nt); });
-    memcpy(d, s, len / nt);
-    for (auto& t : th) t.join();
-  }
-  return 0;
-}
-}  // namespace
-
-int itr_forward_loglik_host(itr_model_t m, itr_plan_t p, const uint16_t* h_obs,
-                            double* h_ll) {
-  if (int e = check_plan(p)) return e;
-  if (p->nblocks == 0) return 0;
-  if ((!h_obs && p->total) || !h_ll) return fail(ITR_EINVAL, "null host pointer");
-  DevBuf o, l;
-  HIP_TRY(hipMalloc(&o.p, std::max<int64_t>(p->total, 1) * sizeof(uint16_t)));
-  HIP_TRY(hipMalloc(&l.p, p->nblocks * sizeof(double)));
-  if (p->total)
-    HIP_TRY(hipMemcpy(o.p, h_obs, p->total * sizeof(uint16_t), hipMemcpyHostToDevice));
-  if (int e = itr_forward_loglik(m, p, (const uint16_t*)o.p, (double*)l.p, nullptr)) return e;
-  HIP_TRY(hipMemcpy(h_ll, l.p, p->nblocks * sizeof(double), hipMemcpyDeviceToHost));
-  return 0;
-}
-
-int itr_viterbi_host(itr_model_t m, itr_plan_t p, const uint16_t* h_obs, uint8_t* h_path) {
-  if (int e = check_plan(p)) return e;
-  if (p->total == 0) return 0;
-  if (!h_obs || !h_path) return fail(ITR_EINVAL, "null host pointer");
-  DevBuf o, y;
-  HIP_TRY(hipMalloc(&o.p, p->total * sizeof(uint16_t)));
-  HIP_TRY(hipMalloc(&y.p, p->total));
-  HIP_TRY(hipMemcpy(o.p, h_obs, p->total * sizeof(uint16_t), hipMemcpyHostToDevice));
-  if (int e = itr_viterbi(m, p, (const uint16_t*)o.p, (uint8_t*)y.p, nullptr)) return e;
-  HIP_TRY(hipMemcpy(h_path, y.p, p->total, hipMemcpyDeviceToHost));
-  return 0;
-}
-
-int itr_posterior_host(itr_model_t m, itr_plan_t p, const uint16_t* h_obs, double* h_post) {
-  if (int e = check_model(m)) return e;
-  if (int e = check_plan(p)) return e;
-  if (p->total == 0) return 0;
-  if (!h_obs || !h_post) return fail(ITR_EINVAL, "null host pointer");
-  DevBuf o, y;
-  const size_t bytes = (size_t)p->total * m->n * sizeof(double);
-  HIP_TRY(hipMalloc(&o.p, p->total * sizeof(uint16_t)));
-  HIP_TRY(hipMalloc(&y.p, bytes));
-  HIP_TRY(hipMemcpy(o.p, h_obs, p->total * sizeof(uint16_t), hipMemcpyHostToDevice));
-  if (int e = itr_posterior(m, p, (const uint16_t*)o.p, (double*)y.p, nullptr)) return e;
-  return copy_out_large(h_post, y.p, bytes);
-}
-
 int itr_release_streams(void) {
   g_parts.release();
-  return 0;
-}
-
-int itr_release_staging(void) {
-  g_stage.release();
-  g_hio.release();
-  itr::release_vanloan_workspace();
   return 0;
 }
 
@@ -2336,282 +1401,6 @@ int itr_emission_rows(int n_states, const double* tables, double* out, void* str
   if (!tables || !out) return fail(ITR_EINVAL, "null device pointer");
   const hipError_t e = itr::launch_emission(n_states, tables, out, (hipStream_t)stream);
   if (e != hipSuccess) return fail(ITR_EHIP, "emission launch failed: %s", hipGetErrorString(e));
-  return 0;
-}
-
-struct itr_maf {
-  itr::MafResult r;
-};
-
-int itr_maf_open(const char* path, const char* const* species, const char* ref,
-                 itr_maf_t* out) {
-  if (!out) return fail(ITR_EINVAL, "null output pointer");
-  *out = nullptr;
-  if (!path || !species) return fail(ITR_EINVAL, "null path or species list");
-  for (int k = 0; k < 4; ++k)
-    if (!species[k]) return fail(ITR_EINVAL, "species list needs 4 names");
-  auto* h = new itr_maf();
-  std::string err;
-  const int rc = itr::maf_read(path, species, ref, &h->r, &err);
-  if (rc) {
-    delete h;
-    return fail(rc == 2 ? ITR_EDATA : ITR_EINVAL, "%s", err.c_str());
-  }
-  *out = h;
-  return 0;
-}
-
-int itr_maf_sizes(itr_maf_t h, int64_t* n_blocks, int64_t* n_columns, int64_t* n_coord_blocks,
-                  int64_t* n_coords) {
-  if (!h) return fail(ITR_EINVAL, "null MAF handle");
-  if (n_blocks) *n_blocks = (int64_t)h->r.off.size() - 1;
-  if (n_columns) *n_columns = (int64_t)h->r.obs.size();
-  if (n_coord_blocks) *n_coord_blocks = (int64_t)h->r.coord_off.size() - 1;
-  if (n_coords) *n_coords = (int64_t)h->r.coords.size();
-  return 0;
-}
-
-int itr_maf_copy(itr_maf_t h, uint16_t* obs, int64_t* block_off, int64_t* coords,
-                 int64_t* coord_off) {
-  if (!h) return fail(ITR_EINVAL, "null MAF handle");
-  const auto& r = h->r;
-  if (obs && !r.obs.empty()) memcpy(obs, r.obs.data(), r.obs.size() * sizeof(uint16_t));
-  if (block_off) memcpy(block_off, r.off.data(), r.off.size() * sizeof(int64_t));
-  if (coords && !r.coords.empty()) memcpy(coords, r.coords.data(), r.coords.size() * sizeof(int64_t));
-  if (coord_off) memcpy(coord_off, r.coord_off.data(), r.coord_off.size() * sizeof(int64_t));
-  return 0;
-}
-
-int itr_maf_close(itr_maf_t h) {
-  delete h;
-  return 0;
-}
-
-// V_lst -> (uint16 columns, int64 offsets): the blocks are split into contiguous ranges of
-// about equal column count, one per thread; each thread converts and range-checks its own
-// blocks, and the first bad symbol (lowest block) is reported.
-namespace {
-// V_lst -> uint16 columns at the given offsets: the blocks are split into contiguous ranges
-// of about equal column count, one per thread; each thread converts and range-checks its
-// own blocks, and the first bad symbol (lowest block) is reported.
-// Blocks [0, n_blocks) of the given arrays (block_off absolute: obs + block_off[k] is block
-// k's first column; k_base = the first block's index in messages).
-int pack_blocks(const int64_t* const* blocks, const int64_t* lens, const int64_t* block_off,
-                int64_t n_blocks, uint16_t* obs, int64_t k_base = 0) {
-  const int64_t c_begin = block_off[0], total = block_off[n_blocks] - c_begin;
-  if (total == 0) return 0;
-  const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, total >> 18));
-  std::vector<int64_t> bad(nt, -1), bad_col(nt, -1);
-  parallel_for(nt, [&](int w) {
-    const int64_t lo_col = c_begin + total * w / nt, hi_col = c_begin + total * (w + 1) / nt;
-    // blocks whose first column falls in [lo_col, hi_col)
-    int64_t k = std::lower_bound(block_off, block_off + n_blocks, lo_col) - block_off;
-    for (; k < n_blocks && block_off[k] < hi_col; ++k) {
-      const int64_t* src = blocks[k];
-      uint16_t* dst = obs + block_off[k];
-      const int64_t len = lens[k];
-      int64_t ok = 1;
-      for (int64_t t = 0; t < len; ++t) {
-        const int64_t v = src[t];
-        ok &= (uint64_t)v < (uint64_t)ITR_NOBS;
-        dst[t] = (uint16_t)v;
-      }
-      if (!ok) {
-        int64_t t = 0;
-        while ((uint64_t)src[t] < (uint64_t)ITR_NOBS) ++t;
-        bad[w] = k;
-        bad_col[w] = t;
-        return;
-      }
-    }
-  });
-  for (int w = 0; w < nt; ++w)
-    if (bad[w] >= 0)
-      return fail(ITR_EDATA, "observed symbol %lld (block %lld, column %lld) outside the "
-                  "625-letter alphabet", (long long)blocks[bad[w]][bad_col[w]],
-                  (long long)(k_base + bad[w]), (long long)bad_col[w]);
-  return 0;
-}
-
-
-// the blocks of a host-block call against the plan's layout; packed into pinned memory and
-// copied to the device buffer (stream order on the null stream, like the sweeps after it)
-int upload_blocks(itr_plan_t p, const int64_t* const* blocks, const int64_t* lens,
-                  int64_t n_blocks, size_t extra_dev, uint16_t** d_obs) {
-  if (n_blocks != p->nblocks)
-    return fail(ITR_EINVAL, "%lld blocks for a plan of %lld", (long long)n_blocks,
-                (long long)p->nblocks);
-  if (n_blocks > 0 && !lens) return fail(ITR_EINVAL, "null lengths");
-  for (int64_t k = 0; k < n_blocks; ++k) {
-    if (lens[k] != p->h_off[k + 1] - p->h_off[k])
-      return fail(ITR_EINVAL, "block %lld has %lld columns, the plan %lld", (long long)k,
-                  (long long)lens[k], (long long)(p->h_off[k + 1] - p->h_off[k]));
-    if (lens[k] > 0 && !blocks[k]) return fail(ITR_EINVAL, "block %lld is null", (long long)k);
-  }
-  const size_t ob = (size_t)std::max<int64_t>(p->total, 1) * sizeof(uint16_t);
-  const size_t ob16 = (ob + 255) & ~(size_t)255;
-  if (int e = g_hio.reserve(std::max(ob, (size_t)p->total), ob16 + extra_dev)) return e;
-  uint16_t* h = (uint16_t*)g_hio.pin;
-  *d_obs = (uint16_t*)g_hio.dbuf;
-  // two halves (by blocks): the first half's copy runs while the second is packed
-  const int64_t kh = std::lower_bound(p->h_off.begin(), p->h_off.end() - 1, p->total / 2) -
-                     p->h_off.begin();
-  const int64_t cuts[3] = {0, std::min<int64_t>(kh, n_blocks), n_blocks};
-  for (int part = 0; part < 2; ++part) {
-    const int64_t k0 = cuts[part], k1 = cuts[part + 1];
-    if (k1 <= k0) continue;
-    if (int e = pack_blocks(blocks + k0, lens + k0, p->h_off.data() + k0, k1 - k0, h, k0))
-      return e;
-    const int64_t c0 = p->h_off[k0], c1 = p->h_off[k1];
-    if (c1 > c0)
-      HIP_TRY(hipMemcpyAsync(*d_obs + c0, h + c0, (c1 - c0) * sizeof(uint16_t),
-                             hipMemcpyHostToDevice, g_hio.st));
-  }
-  return 0;
-}
-size_t dev_tail(itr_plan_t p) {  // first byte after the observations in g_hio.dbuf
-  const size_t ob = (size_t)std::max<int64_t>(p->total, 1) * sizeof(uint16_t);
-  return (ob + 255) & ~(size_t)255;
-}
-}  // namespace
-
-int itr_pack_symbols(const int64_t* const* blocks, const int64_t* lens, int64_t n_blocks,
-                     uint16_t* obs, int64_t* block_off) {
-  if (n_blocks < 0 || !block_off || (n_blocks > 0 && !lens))
-    return fail(ITR_EINVAL, "bad pack arguments");
-  block_off[0] = 0;
-  for (int64_t k = 0; k < n_blocks; ++k) {
-    if (lens[k] < 0) return fail(ITR_EINVAL, "block %lld has negative length", (long long)k);
-    if (lens[k] > 0 && !blocks[k]) return fail(ITR_EINVAL, "block %lld is null", (long long)k);
-    block_off[k + 1] = block_off[k] + lens[k];
-  }
-  if (block_off[n_blocks] == 0) return 0;
-  if (!obs) return fail(ITR_EINVAL, "null output");
-  return pack_blocks(blocks, lens, block_off, n_blocks, obs);
-}
-
-namespace {
-// ITR_HOST_TIMING=1: stage times of the host-block entry points on stderr (diagnostics)
-struct HostClock {
-  bool on = getenv("ITR_HOST_TIMING") != nullptr;
-  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-  void lap(const char* what) {
-    if (!on) return;
-    (void)hipDeviceSynchronize();
-    const auto now = std::chrono::steady_clock::now();
-    fprintf(stderr, "%s %.3f ms  ", what, std::chrono::duration<double, std::milli>(now - t).count());
-    t = now;
-  }
-  void end() {
-    if (on) fprintf(stderr, "\n");
-  }
-};
-}  // namespace
-
-int itr_forward_loglik_blocks(itr_model_t m, itr_plan_t p, const int64_t* const* blocks,
-                              const int64_t* lens, int64_t n_blocks, double* h_ll) {
-  if (int e = check_model(m)) return e;
-  if (int e = check_plan(p)) return e;
-  if (p->nblocks > 0 && !h_ll) return fail(ITR_EINVAL, "null output");
-  uint16_t* d_obs = nullptr;
-  const size_t tail = dev_tail(p);
-  HostClock clk;
-  if (int e = upload_blocks(p, blocks, lens, n_blocks, (size_t)p->nblocks * 8 + 8, &d_obs))
-    return e;
-  clk.lap("loglik: pack+h2d");
-  if (p->nblocks == 0) return 0;
-  double* d_ll = (double*)((char*)g_hio.dbuf + tail);
-  if (int e = itr_forward_loglik(m, p, d_obs, d_ll, g_hio.st)) return e;
-  clk.lap("sweep");
-  HIP_TRY(hipMemcpyAsync(h_ll, d_ll, p->nblocks * sizeof(double), hipMemcpyDeviceToHost,
-                         g_hio.st));
-  HIP_TRY(hipStreamSynchronize(g_hio.st));
-  clk.lap("d2h");
-  clk.end();
-  return 0;
-}
-
-int itr_viterbi_blocks(itr_model_t m, itr_plan_t p, const int64_t* const* blocks,
-                       const int64_t* lens, int64_t n_blocks, double* h_path) {
-  if (int e = check_model(m)) return e;
-  if (int e = check_plan(p)) return e;
-  if (p->total > 0 && !h_path) return fail(ITR_EINVAL, "null output");
-  uint16_t* d_obs = nullptr;
-  const size_t tail = dev_tail(p);
-  HostClock clk;
-  if (int e = upload_blocks(p, blocks, lens, n_blocks, (size_t)p->total + 8, &d_obs)) return e;
-  clk.lap("viterbi: pack+h2d");
-  if (p->total == 0) return 0;
-  uint8_t* d_path = (uint8_t*)g_hio.dbuf + tail;
-  if (int e = itr_viterbi(m, p, d_obs, d_path, g_hio.st)) return e;
-  const int64_t total = p->total;
-  const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, total >> 18));
-  // while the device sweeps: host threads map the output's pages (one write per 4 KiB), so
-  // the widening below does not page-fault its way through a fresh 8-bytes-per-column array
-  if (!clk.on)
-    parallel_for(nt, [&](int w) {
-      const int64_t lo = total * w / nt, hi = total * (w + 1) / nt;
-      for (int64_t c = lo; c < hi; c += 512) h_path[c] = 0.0;
-    });
-  clk.lap("sweep");
-  // the states back through the pinned buffer (the observations' upload finished before the
-  // sweep on this stream), widened to float64 (the reference's path dtype) by host threads
-  uint8_t* h = (uint8_t*)g_hio.pin;
-  HIP_TRY(hipMemcpyAsync(h, d_path, p->total, hipMemcpyDeviceToHost, g_hio.st));
-  HIP_TRY(hipStreamSynchronize(g_hio.st));
-  clk.lap("d2h");
-  parallel_for(nt, [&](int w) {
-    const int64_t lo = total * w / nt, hi = total * (w + 1) / nt;
-    for (int64_t c = lo; c < hi; ++c) h_path[c] = (double)h[c];
-  });
-  clk.lap("to_f64");
-  clk.end();
-  return 0;
-}
-
-int itr_format_float(double x, char* out, int cap) {
-  char b[40];
-  const int n = itr::format_pyfloat(x, b);
-  if (!out || cap < n + 1) return fail(ITR_EINVAL, "buffer too small");
-  memcpy(out, b, n);
-  out[n] = 0;
-  return 0;
-}
-
-namespace {
-// per-column reference coordinates must cover exactly the decoded columns: the writers read
-// coords[c] for every column c
-int check_coords(const int64_t* block_off, int64_t n_blocks, const int64_t* coords,
-                 int64_t n_coords) {
-  if (!coords) return 0;
-  const int64_t total = n_blocks > 0 ? block_off[n_blocks] : 0;
-  if (n_coords != total)
-    return fail(ITR_EINVAL, "%lld reference coordinates for %lld decoded columns",
-                (long long)n_coords, (long long)total);
-  return 0;
-}
-}  // namespace
-
-int itr_write_viterbi_csv(const char* path, const uint8_t* states, const int64_t* block_off,
-                          int64_t n_blocks, const int64_t* coords, int64_t n_coords) {
-  if (!path || (n_blocks > 0 && (!states || !block_off)) || n_blocks < 0)
-    return fail(ITR_EINVAL, "bad arguments");
-  if (int e = check_coords(block_off, n_blocks, coords, n_coords)) return e;
-  std::string err;
-  if (itr::write_viterbi_csv(path, states, block_off, n_blocks, coords, &err))
-    return fail(ITR_EINVAL, "%s", err.c_str());
-  return 0;
-}
-
-int itr_write_posterior_csv(const char* path, const double* post, int n_states,
-                            const int64_t* block_off, int64_t n_blocks, const int64_t* coords,
-                            int64_t n_coords, int threads) {
-  if (!path || n_states < 0 || n_blocks < 0 || (n_blocks > 0 && (!post || !block_off)))
-    return fail(ITR_EINVAL, "bad arguments");
-  if (int e = check_coords(block_off, n_blocks, coords, n_coords)) return e;
-  std::string err;
-  if (itr::write_posterior_csv(path, post, n_states, block_off, n_blocks, coords, threads, &err))
-    return fail(ITR_EINVAL, "%s", err.c_str());
   return 0;
 }
 

@@ -289,6 +289,8 @@ PruneVitGeometry prune_vit_geometry(int n) {
   // as many waves (blocks) per CU as the LDS holds beside the matrix, at most 16
   int waves = 16;
   while (waves > 1 && pv_lds(n, waves) > 160 * 1024) --waves;
+  // N = 141..144: the matrix and one wave's rows exceed the 160 KiB of LDS (no layout)
+  if (pv_lds(n, waves) > 160 * 1024) return g;
   g.waves = waves;
   g.block = 64 * waves;
   g.lds = pv_lds(n, waves);

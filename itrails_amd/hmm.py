@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes
 import hashlib
+import os
 import threading
 from collections import OrderedDict
 from typing import Iterable, List, Sequence
@@ -287,11 +288,22 @@ def _posteriors(model: Model, plan: Plan, obs: np.ndarray) -> np.ndarray:
 # the model tables, the Viterbi slot tables and the plan once.  Keys are the contents
 # (a, b, pi bytes; block offsets) and the current device, so a changed input is a new entry;
 # at most two of each are kept (evicted objects are freed when no caller holds them).
+# Models are read-only once built (their Viterbi slot tables are built under a lock in the
+# library), so threads share them; a plan owns its sweep workspaces and work counters, so
+# plans are cached per thread: two threads decoding the same layout never sweep into one
+# plan's counters and rows at the same time.
 # ---------------------------------------------------------------------------------------
 _CACHE_LOCK = threading.Lock()
 _MODELS: "OrderedDict" = OrderedDict()
-_PLANS: "OrderedDict" = OrderedDict()
+_TLS = threading.local()
 _CACHE_SIZE = 2
+
+
+def _thread_plans() -> "OrderedDict":
+    d = getattr(_TLS, "plans", None)
+    if d is None:
+        d = _TLS.plans = OrderedDict()
+    return d
 
 
 def _device_index():
@@ -309,7 +321,7 @@ def _digest(*arrays):
 
 
 def _cache_get(cache, key, make):
-    with _CACHE_LOCK:
+    with _CACHE_LOCK:  # (a per-thread cache needs no lock; one lock keeps this simple)
         obj = cache.get(key)
         if obj is not None:
             cache.move_to_end(key)
@@ -335,21 +347,35 @@ def _cached_model(a, b, pi, decode=False) -> Model:
 
 def _cached_plan(off) -> Plan:
     off = np.ascontiguousarray(off, dtype=np.int64)
-    return _cache_get(_PLANS, (_device_index(), _digest(off)), lambda: Plan(off))
+    return _cache_get(_thread_plans(), (_device_index(), _digest(off)), lambda: Plan(off))
 
 
 def clear_caches():
-    """Drop the wrappers' cached models and plans (their device memory is freed when no
-    caller holds them)."""
+    """Drop the wrappers' cached models and the calling thread's cached plans (their device
+    memory is freed when no caller holds them)."""
     with _CACHE_LOCK:
         _MODELS.clear()
-        _PLANS.clear()
+        _thread_plans().clear()
 
 
-try:  # the V_lst scan in C (csrc/blocks_ext.c, built with the library)
-    from . import _blocks as _blocks_ext
-except ImportError:  # (argument marshalling only: the Python scan below does the same)
-    _blocks_ext = None
+def _load_blocks_ext():
+    """The V_lst scan in C (csrc/blocks_ext.c, built with the library); ITR_BLOCKS_EXT names
+    another build of it (the sanitizer build of scripts/asan_host.sh)."""
+    path = os.environ.get("ITR_BLOCKS_EXT")
+    if path:
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("itrails_amd._blocks", path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod
+    try:
+        from . import _blocks
+        return _blocks
+    except ImportError:  # (argument marshalling only: the Python scan below does the same)
+        return None
+
+
+_blocks_ext = _load_blocks_ext()
 
 
 def _lens_ptrs(V_lst):

@@ -384,3 +384,23 @@ def test_hybrid_posterior_split_blocks(gpu, golden_name, n):
     assert _posterior_every_block(t, obs, off, post, chunk_cols=100_000) == off[-1]
     del post, post0, d_obs
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n", [137, 141])
+def test_short_blocks_pruned_viterbi_layout_limits(gpu, n):
+    """N = 137 and 141 in the pruned Viterbi's regime (many short blocks): its layout holds
+    only two blocks per CU beside the matrix at N = 137 and does not fit the 160 KiB of LDS
+    at N = 141, so itr_viterbi / itr_forward_viterbi must take the 9-wave layout instead of
+    failing the launch; every path against the CPU restatement."""
+    import torch
+    from test_gpu_sweeps import random_hmm
+    a, b, pi = random_hmm(np.random.default_rng(n), n)
+    lengths = block_lengths(np.random.default_rng(2), 200_000, 300.0)
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=n)
+    assert len(lengths) > 2 * 256 and off[-1] / len(lengths) <= 400
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).cuda()
+    path = hmm.viterbi_device(model, plan, d_obs).cpu().numpy()
+    ll, path2 = hmm.forward_viterbi_device(model, plan, d_obs)
+    assert np.array_equal(path2.cpu().numpy(), path)
+    _check_all_blocks(build_tables(a, b, pi), obs, off, ll.cpu().numpy(), path)
