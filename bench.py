@@ -38,6 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_SPEC_TFLOPS = 78.6  # MI355X FP64 vector / matrix (AMD spec, FMA counted as 2 flop)
+FP64_SPEC_ADDMAX_TOPS = FP64_SPEC_TFLOPS / 2  # one f64 add or max per lane per issue slot
 
 # KAT parameters, internal units of the {t_1} case: times and N times mu,
 # r over mu (workflow_optimize.py:360-380)
@@ -668,39 +669,54 @@ def main():
     if rank == 0:
         cols_total = W["cols_total"]
         cols_local = W["cols_local"]
-        fma_peak, am_peak, peak_src = valu_peaks()
+        fma_meas, am_meas, peak_src = valu_peaks()
+        fma_peak, am_peak = FP64_SPEC_TFLOPS, FP64_SPEC_ADDMAX_TOPS
         fwd_avg = float(np.mean(fwd_ms)) if fwd_ms else 0.0
         vit_avg = float(np.mean(vit_ms)) if vit_ms else 0.0
         tb_avg = float(np.mean(tb_ms)) if tb_ms else 0.0
         pair_ops = 2.0 * n * n  # per column: N^2 FMA (forward / backward) or N^2 add + N^2 max
         step_ms = dt / args.steps * 1e3
         fv_avg = float(np.mean(fv_ms)) if fv_ms else 0.0
+        def ideal(fma, am):  # the step's ideal time at the given FP64 rates
+            if args.mode == "fv":
+                return pair_ops * cols_local / (fma * 1e12) * 1e3 + \
+                    pair_ops * cols_local / (am * 1e12) * 1e3
+            if vit_mode:
+                return pair_ops * cols_local / (am * 1e12) * 1e3
+            if post_mode:
+                return 2 * pair_ops * cols_local / (fma * 1e12) * 1e3
+            return pair_ops * cols_local / (fma * 1e12) * 1e3
+        ideal_meas_ms = ideal(fma_meas, am_meas)
         if args.mode == "fv":
             # the timed call itself (itr_forward_viterbi, fork to join): its ideal time at
-            # the VALU peaks, forward at the FMA rate and Viterbi at the add+max rate
-            ideal_ms = pair_ops * cols_local / (fma_peak * 1e12) * 1e3 + \
-                pair_ops * cols_local / (am_peak * 1e12) * 1e3
+            # the FP64 spec rates, forward at the FMA rate and Viterbi at the add+max rate
+            ideal_ms = ideal(fma_peak, am_peak)
             dom = ("itr_forward_viterbi: hybrid_sweep_kernel<FWD_LL> (forward VALU halves, "
-                   "reserved CUs) | sweep_kernel<VIT> (longest blocks, reserved CUs) | "
+                   "reserved CUs) | vit_group_kernel (longest blocks' Viterbi, reserved CUs) | "
                    "wave_mixed_kernel (forward groups + per-wave Viterbi, the rest)")
             dom_ms = float(np.mean(loop_ms)) if loop_ms else (fv_avg if fv_avg else vit_avg)
             dom_peak = 2 * pair_ops * cols_local / (ideal_ms * 1e-3) / 1e12  # combined peak
             dom_mode = 3
         elif vit_mode:
-            dom, dom_ms, dom_peak, dom_mode = ("Viterbi max-plus sweep: sweep_kernel<VIT> (longest "
+            dom, dom_ms, dom_peak, dom_mode = ("Viterbi max-plus sweep: vit_group_kernel (longest "
                                                "blocks, both reserved CU sets) | wave_vit_kernel "
                                                "(rest)"), \
                 float(np.mean(loop_ms)) if loop_ms else vit_avg, am_peak, 3
-            ideal_ms = pair_ops * cols_local / (am_peak * 1e12) * 1e3
+            ideal_ms = ideal(fma_peak, am_peak)
         elif post_mode:
-            dom, dom_ms, dom_peak, dom_mode = "sweep_kernel<BWD> (backward + posterior)", vit_avg, \
-                fma_peak, 2
-            ideal_ms = 2 * pair_ops * cols_local / (fma_peak * 1e12) * 1e3
+            # the whole itr_posterior step (forward-store launch + backward launch, 4 N^2
+            # flop per column) against the FMA peak
+            hyb = 65 <= n <= 72 or 129 <= n <= 144  # (mfma_sweeps.hip kMCfgs: post = true)
+            dom = ("itr_posterior: hybrid_sweep_kernel<FWD_STORE> + hybrid_sweep_kernel<BWD> "
+                   "(matrix-core groups + VALU tasks of the longest blocks)") if hyb else \
+                ("itr_posterior: sweep_kernel<FWD_STORE> + sweep_kernel<BWD> (VALU)")
+            dom_ms, dom_peak, dom_mode = step_ms, fma_peak, 2
+            ideal_ms = ideal(fma_peak, am_peak)
         else:
             dom, dom_ms, dom_peak, dom_mode = "sweep_kernel<FWD_LL> (forward)", fwd_avg, \
                 fma_peak, 0
-            ideal_ms = pair_ops * cols_local / (fma_peak * 1e12) * 1e3
-        dom_ops = (2 if args.mode == "fv" else 1) * pair_ops * cols_local
+            ideal_ms = ideal(fma_peak, am_peak)
+        dom_ops = (2 if args.mode in ("fv", "posterior") else 1) * pair_ops * cols_local
         achieved = dom_ops / (dom_ms * 1e-3) / 1e12 if dom_ms else 0.0
         default_fv = args.mode == "fv" and n == 70 and not intro and kind == "chr10" and \
             args.block_len == 0 and args.mbp is None  # (the profiled command's workload)
@@ -782,10 +798,15 @@ def main():
                                                                         "FP64 VALU FMA"),
                          "achieved": round(achieved, 4), "peak": round(dom_peak, 3),
                          "unit": "TFLOP/s", "frac": round(achieved / dom_peak, 5),
-                         "peak_source": peak_src,
-                         "peak_fma_tflops": round(fma_peak, 3),
-                         "peak_add_max_tops": round(am_peak, 3),
+                         "peak_source": "AMD spec: FP64 78.6 TFLOP/s (FMA), 39.3 T add/max "
+                                        "ops/s",
                          "peak_spec_tflops": FP64_SPEC_TFLOPS,
+                         "peak_spec_add_max_tops": FP64_SPEC_ADDMAX_TOPS,
+                         "frac_vs_measured_peaks": round(ideal_meas_ms / dom_ms, 5)
+                         if dom_ms else None,
+                         "measured_peaks": {"fma_tflops": round(fma_meas, 3),
+                                            "add_max_tops": round(am_meas, 3),
+                                            "source": peak_src},
                          "traffic": traffic, "traffic_note": traffic_note,
                          "kernel_ms": round(dom_ms, 4),
                          "kernel_ms_source": ("HIP events of the timed call in the timed loop "

@@ -409,6 +409,32 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
   return 0;
 }
 
+// The forward's VALU tasks alone (the plan's urgent tasks: the longest blocks and the split
+// ones' halves, v.tasks / v.nblocks) on `st`, at most max_grid at a time: on lane groups
+// (lane_groups.h, ~35 VALU instructions per column on one wave per SIMD) where that layout
+// exists for the state count, else the hybrid launch's VALU part.  The work counter
+// (d_queue[3]) must be zero.
+int run_valu_forward(itr_model_t m, itr_plan_t p, itr::SweepArgs v, const itr::MfmaGeometry& g,
+                     hipStream_t st, int64_t max_grid, bool share_cu) {
+  const itr::FwdGroupGeometry fg = itr::fwd_group_geometry(m->n);
+  bool groups = fg.block > 0 && fg.xr == g.xr;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_NO_FWD_GROUPS")) groups = false;
+#endif
+  if (groups) {
+    v.queue = p->d_queue + 3;
+    v.prio_len = 0;
+    itr::FwdGroupGeometry gx = fg;
+    const int64_t grid = std::min<int64_t>(max_grid, v.nblocks);
+    if (grid <= 0) return 0;
+    if (!share_cu) gx.lds = std::max(gx.lds, itr::kExclusiveLds);  // one per CU
+    HIP_TRY(itr::launch_fwd_group(gx, (int)grid, v, st));
+    return 0;
+  }
+  return run_hybrid(itr::MODE_FWD_LL, m, p, v, g, st, nullptr, true, false, max_grid, false, 0,
+                    share_cu);
+}
+
 int forward_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* loglik,
                  hipStream_t st, int cus);
 
@@ -573,9 +599,41 @@ int forward_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* logli
   if (g.cfg >= 0 && p->ngroups_ll > 0) {
     a.tasks = p->d_utasks;
     a.nblocks = p->nutasks;
-    if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, st, "forward", true, true, -1, true,
-                           cus))
+    const itr::FwdGroupGeometry fgeo = itr::fwd_group_geometry(m->n);
+    bool part = cus == 0 && p->nutasks > 0 && fgeo.block > 0 && fgeo.xr == g.xr;
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_NO_FWD_GROUPS")) part = false;
+#endif
+    if (part) {
+      // The VALU tasks (the longest blocks' halves) one per reserved CU on the lane-group
+      // layout, the matrix-core groups on the other CUs; the reserved CUs join the groups when
+      // their task is done.  The set: one CU per task, in whole XCC sets, at most a quarter of
+      // the chip (masked streams: a group workgroup beside a running half slows it down)
+      const int ncu = cu_count();
+      const int X = (ncu % 8 == 0) ? 8 : 1;
+      const int rfr = (int)std::min<int64_t>((p->nutasks + X - 1) / X * X, ncu / 4);
+      Partition* pt = nullptr;
+      if (int e = partition(0, rfr, &pt)) return e;
+      Scope sc("forward", st);
+      HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
+      HIP_TRY(hipEventRecord(pt->fork, st));
+      HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
+      HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
+      if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->blk, nullptr, false, true,
+                             (int64_t)g.per_cu * (ncu - rfr), false, ncu - rfr))
+        return e;
+      if (int e = run_valu_forward(m, p, a, g, pt->lng2, rfr, false)) return e;
+      if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->lng2, nullptr, false, true,
+                             (int64_t)g.per_cu * rfr, false, rfr))
+        return e;
+      HIP_TRY(hipEventRecord(pt->jl2, pt->lng2));
+      HIP_TRY(hipEventRecord(pt->jb, pt->blk));
+      HIP_TRY(hipStreamWaitEvent(st, pt->jl2, 0));
+      HIP_TRY(hipStreamWaitEvent(st, pt->jb, 0));
+    } else if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, st, "forward", true, true, -1,
+                                  true, cus)) {
       return e;
+    }
     HIP_TRY(itr::launch_fwd_split_combine(m->n, g.xr, (int)p->nhsplit, p->d_hsplit_blk,
                                           p->d_svec, p->d_sK, loglik, st));
     return 0;
@@ -722,6 +780,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   a.emit = m->LE;
   a.init = m->LPIE;
   a.queue = p->d_queue + 2;  // own counter: may run concurrently with a forward sweep
+  a.xrec = vit_stride(m->n);  // (the record stride every Viterbi layout of this call writes)
   a.alpha = p->d_alpha;
   a.stay = p->d_stay;
   a.last_state = p->d_last;
@@ -916,9 +975,7 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
       }
       if (split_fwd) {
         const int64_t fg = (int64_t)p->fwd_per_cu * rfr;  // forward halves at a time on the set
-        if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, af, gf, pt->lng2, nullptr, true, false,
-                               fg, false, 0, fg > rfr))
-          return e;
+        if (int e = run_valu_forward(m, p, af, gf, pt->lng2, fg, fg > rfr)) return e;
       }
     } else if (mixed) {
       if (int e = launch_bulk()) return e;

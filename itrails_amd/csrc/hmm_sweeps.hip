@@ -47,6 +47,7 @@
 
 #include "valu_sweep.h"
 #include "trace.h"
+#include "lane_groups.h"
 
 namespace itr {
 
@@ -54,6 +55,20 @@ template <int QL, int WV, int RJN, int IQ, int MODE>
 __global__ void __launch_bounds__(64 * WV, (Occ<QL, WV, RJN, IQ, MODE>::value))
     sweep_kernel(SweepArgs p) {
   sweep_device<QL, WV, RJN, IQ, MODE>(p);
+}
+
+// Viterbi on small lane groups per target (lane_groups.h); the register budget holds at least
+// two waves per SIMD (four-wave workgroups: two per CU, the planner pairs long blocks on a
+// reserved CU) and every wave of one workgroup
+template <int G, int W, int S>
+__global__ void __launch_bounds__(64 * W, ((W + 3) / 4 > 2 ? (W + 3) / 4 : 2))
+    vit_group_kernel(SweepArgs p) {
+  vit_group_device<G, W, S>(p);
+}
+template <int G, int W, int S>
+__global__ void __launch_bounds__(64 * W, ((W + 3) / 4 > 2 ? (W + 3) / 4 : 2))
+    fwd_group_kernel(SweepArgs p) {
+  fwd_group_device<G, W, S>(p);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -81,7 +96,7 @@ __global__ void __launch_bounds__(256) vit_trace_kernel(TraceArgs p) {
 // ---------------------------------------------------------------------------------------
 struct Cfg {
   int ql, w, rj, iq;  // lanes per target, waves, target states per lane, sources per lane
-};
+};                    // (ql < 0: Viterbi on lane groups of -ql lanes, lane_groups.h)
 static constexpr Cfg kCfgs[] = {
     // eight lanes per target, four waves (one per SIMD), several targets per lane: fewest
     // LDS reads per column, several workgroups per CU
@@ -93,12 +108,22 @@ static constexpr Cfg kCfgs[] = {
     // four lanes per target: one DPP combine stage less and twice the pairs per lane
     {4, 4, 1, 16}, {4, 5, 1, 18}, {4, 6, 1, 24}, {4, 9, 1, 34}, {4, 3, 2, 24}, {4, 4, 2, 32},
     // eight lanes per target, three targets per lane, W = ceil(N / 24) waves
-    {8, 3, 3, 9}, {8, 6, 3, 17}};
+    {8, 3, 3, 9}, {8, 6, 3, 17},
+    // Viterbi only, lane groups (lane_groups.h): three lanes per target and 20 targets per wave
+    // (N <= 72), five lanes per target and 12 targets per wave (N <= 140 / 150)
+    {-3, 4, 1, 24}, {-5, 12, 1, 28}, {-5, 12, 1, 30},
+    // eight lanes per target, three targets per lane, six waves, 144 sources (N <= 144)
+    {8, 6, 3, 18}};
 static constexpr int kNarrow = 7;  // entries 0..6
 [[maybe_unused]] static constexpr int kNumCfgs = (int)(sizeof kCfgs / sizeof kCfgs[0]);
 
-static int cfg_xr(int c) { return (64 / kCfgs[c].ql) * kCfgs[c].w * kCfgs[c].rj; }
-static bool fits(int c, int n) { return cfg_xr(c) >= n && kCfgs[c].ql * kCfgs[c].iq >= n; }
+static int cfg_xr(int c) {
+  if (kCfgs[c].ql < 0) return 4 * (16 / -kCfgs[c].ql) * kCfgs[c].w;  // lane groups
+  return (64 / kCfgs[c].ql) * kCfgs[c].w * kCfgs[c].rj;
+}
+static bool fits(int c, int n) {
+  return cfg_xr(c) >= n && (kCfgs[c].ql < 0 ? -kCfgs[c].ql : kCfgs[c].ql) * kCfgs[c].iq >= n;
+}
 
 // Measured on the (5,5) model (N = 70), 10 Mbp: the forward log-likelihood
 // sweep runs fastest on three waves with three targets per lane (configuration 20), the
@@ -113,19 +138,26 @@ static int pick_cfg(int n, int mode) {
     if (c >= 0 && c < kNumCfgs && fits(c, n)) return c;
   }
 #endif
+  int c = -1;
   // (posterior sweeps at N = 70 on configuration 20: 465 -> 496 M columns/s,
   // scripts/gpu_cfgsmall.sh)
-  if (n > 64 && n <= 72) return mode == MODE_VIT ? 9 : 20;
+  if (n > 64 && n <= 72) c = mode == MODE_VIT ? 22 : 20;
   // Viterbi at 32 < N <= 64 on eight waves, one target per lane ((4,4) model, N = 46:
   // 7.3 -> 6.2 ms)
-  if (n > 32 && n <= 64 && mode == MODE_VIT) return 8;
+  else if (n > 32 && n <= 64 && mode == MODE_VIT) c = 8;
   // measured on the (7,7) model (N = 133, 10 Mbp, scripts/gpu_cfg133.sh): six waves with
-  // three targets per lane for the probability sweeps (posterior 146 -> 175 M columns/s),
-  // nine waves with four lanes per target for Viterbi (40.7 -> 26.0 ms)
-  if (n > 128 && n <= 144) return mode == MODE_VIT ? 17 : 21;
+  // three targets per lane for the probability sweeps (posterior 146 -> 175 M columns/s);
+  // Viterbi on lane groups of five, twelve waves (three per SIMD): 23.4 against 25.4 ms for
+  // nine waves with four lanes per target (configuration 17: three waves on SIMD 0) and 27.6
+  // for groups of three on seven waves (profiles/r6b_vit_layouts.txt)
+  else if (n > 128 && n <= 144)
+    c = mode == MODE_VIT ? (n <= 140 ? 23 : 24) : (n <= 136 ? 21 : 25);
   // introgression (5,5) model, N = 95 (scripts/gpu_cfg95.sh): Viterbi on six waves with four
-  // lanes per target (11.9 -> 11.0 ms); the probability sweeps keep configuration 3
-  if (n > 72 && n <= 96 && mode == MODE_VIT) return 16;
+  // lanes per target (11.9 -> 11.0 ms; 10.4 against 14.8 ms for lane groups of five on eight
+  // waves, profiles/r6b_vit_layouts.txt); the probability sweeps keep configuration 3
+  else if (n > 72 && n <= 96 && mode == MODE_VIT) c = 16;
+  // every choice must cover the state count (targets and sources), else the generic ones
+  if (c >= 0 && fits(c, n)) return c;
   for (int c = 0; c < kNarrow; ++c)
     if (fits(c, n)) return c;
   return -1;
@@ -133,6 +165,10 @@ static int pick_cfg(int n, int mode) {
 
 static size_t lds_bytes(int cfg, int mode) {
   const int w = kCfgs[cfg].w, iq = kCfgs[cfg].iq;
+  if (kCfgs[cfg].ql < 0)
+    return (size_t)2 * (-kCfgs[cfg].ql * iq + 64) * sizeof(double) + 5 * 64 * sizeof(double) +
+           (size_t)2 * VIT_TILE * cfg_xr(cfg) * sizeof(double) + 32 * sizeof(int) +
+           (size_t)2 * 64 * w * sizeof(uint16_t);
   const int xs = kCfgs[cfg].ql * (iq + (iq & 1));
   const int xr = cfg_xr(cfg);
   const int tb = 64 * w;
@@ -157,9 +193,33 @@ static int occ_one(size_t lds) {
   return nb > 0 ? nb : 1;
 }
 
+template <int G, int W, int S>
+static hipError_t dispatch_group(bool launch, const SweepArgs* a, int grid, size_t lds,
+                                 hipStream_t st, int* occ) {
+  static_assert(VitGroupLayout<G, W, S>::XR > 0, "layout");
+  if (launch) {
+    hipLaunchKernelGGL((vit_group_kernel<G, W, S>), dim3(grid), dim3(64 * W), lds, st, *a);
+    return hipGetLastError();
+  }
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, vit_group_kernel<G, W, S>, 64 * W, lds) !=
+      hipSuccess)
+    nb = 1;
+  *occ = nb > 0 ? nb : 1;
+  return hipSuccess;
+}
+
 template <int MODE>
 static hipError_t dispatch(int cfg, bool launch, const SweepArgs* a, int grid, size_t lds,
                            hipStream_t st, int* occ) {
+  if (kCfgs[cfg].ql < 0 && MODE != MODE_VIT) return hipErrorInvalidValue;
+  if constexpr (MODE == MODE_VIT) {
+    switch (cfg) {
+      case 22: return dispatch_group<3, 4, 24>(launch, a, grid, lds, st, occ);
+      case 23: return dispatch_group<5, 12, 28>(launch, a, grid, lds, st, occ);
+      case 24: return dispatch_group<5, 12, 30>(launch, a, grid, lds, st, occ);
+    }
+  }
 #define ITR_CFG(C, QL, WV, RJN, IQ)                                          \
   case C:                                                                    \
     if (launch) return launch_one<QL, WV, RJN, IQ, MODE>(*a, grid, lds, st); \
@@ -188,6 +248,7 @@ static hipError_t dispatch(int cfg, bool launch, const SweepArgs* a, int grid, s
     ITR_CFG(19, 4, 4, 2, 32)
     ITR_CFG(20, 8, 3, 3, 9)
     ITR_CFG(21, 8, 6, 3, 17)
+    ITR_CFG(25, 8, 6, 3, 18)
   }
 #undef ITR_CFG
   return hipErrorInvalidValue;
@@ -224,6 +285,30 @@ SweepGeometry sweep_geometry(int n, int mode) {
   if (pcu && atoi(pcu) > 0) g.per_cu = atoi(pcu);
 #endif
   return g;
+}
+
+// the forward's VALU tasks on lane groups: N = 65..72 (groups of three, four waves, the
+// hybrid forward's 80-wide split vectors)
+FwdGroupGeometry fwd_group_geometry(int n) {
+  FwdGroupGeometry g{};
+  if (n < 65 || n > 72) return g;
+  using L = VitGroupLayout<3, 4, 24>;
+  g.block = L::TB;
+  g.xr = L::XR;
+  g.lds = L::lds_bytes;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fwd_group_kernel<3, 4, 24>, L::TB,
+                                                   g.lds) != hipSuccess)
+    nb = 1;
+  g.per_cu = nb > 0 ? nb : 1;
+  return g;
+}
+
+hipError_t launch_fwd_group(const FwdGroupGeometry& g, int grid, const SweepArgs& a,
+                            hipStream_t st) {
+  if (g.block != 256 || grid <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((fwd_group_kernel<3, 4, 24>), dim3(grid), dim3(g.block), g.lds, st, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_sweep(int mode, const SweepGeometry& g, int grid, const SweepArgs& a,

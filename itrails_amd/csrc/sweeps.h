@@ -61,6 +61,8 @@ struct SweepArgs {
   const int32_t* tasks;         // MODE_FWD_LL: [nblocks x 3] {block, split, slot}, see capi.cpp
   double* svec;                 // MODE_FWD_LL: [nsplit x 2 x XR] vectors of split blocks
   int* sK;                      // MODE_FWD_LL: [nsplit x 2] their power-of-two exponents
+  int xrec;                     // MODE_VIT on the lane-group layout (lane_groups.h): record
+                                //   stride of the checkpoint rows / flag words
   uint64_t* diag;               // diagnostic build only: per-segment cycle sums
   int diag_wave;                // diagnostic build only: the wave that reports
 };
@@ -263,6 +265,20 @@ hipError_t launch_wave_mfma(const WaveMfmaGeometry& g, int grid, const WaveMfmaA
 hipError_t launch_wave_mixed(const WaveMfmaGeometry& g, int grid, const VitArgs& v,
                              const WaveMfmaArgs& f, const int32_t* list, int nlist, int* queue,
                              hipStream_t st, int role = 0);
+
+// The forward log-likelihood's VALU tasks (SweepArgs.tasks: the longest blocks and the
+// halves of the split ones) on lane groups per target (lane_groups.h, hmm_sweeps.hip): their
+// lowest step latency, on the reserved CUs of a partitioned call; xr = the row stride of the
+// split halves' vectors (the hybrid configuration's)
+struct FwdGroupGeometry {
+  int block;    // threads per workgroup (0: no lane-group forward for this state count)
+  int xr;       // target slots = split-vector stride
+  size_t lds;   // dynamic LDS bytes
+  int per_cu;   // resident workgroups per CU
+};
+FwdGroupGeometry fwd_group_geometry(int n);
+hipError_t launch_fwd_group(const FwdGroupGeometry& g, int grid, const SweepArgs& a,
+                            hipStream_t st);
 
 // log-likelihoods of the split blocks of a forward sweep
 hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,

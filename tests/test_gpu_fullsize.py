@@ -404,3 +404,30 @@ def test_short_blocks_pruned_viterbi_layout_limits(gpu, n):
     ll, path2 = hmm.forward_viterbi_device(model, plan, d_obs)
     assert np.array_equal(path2.cpu().numpy(), path)
     _check_all_blocks(build_tables(a, b, pi), obs, off, ll.cpu().numpy(), path)
+
+
+def test_full_size_n27_every_block(gpu):
+    """The reference's example workload (it/examples/example_config.yaml:19-20:
+    n_int_AB = n_int_ABC = 3, N = 27 hidden states; the reference's own (3,3) build,
+    tests/golden/model_kat_3_3.npz) over the config-2 layout (10 Mbp, 5,036 blocks): forward
+    log-likelihoods (1e-8) and Viterbi paths (identical) of every block through the combined
+    and the Viterbi-only call, and every posterior row (1e-8, rows summing to 1)."""
+    import torch
+    g = golden("model_kat_3_3.npz")
+    a, b, pi = g["a"], g["b"], g["pi"]
+    assert a.shape[0] == 27
+    lengths = block_lengths(np.random.default_rng(12345), 10_000_000, 2000.0)
+    obs, off, _ = sample_alignment(a, b, pi, lengths, seed=777)
+    t = build_tables(a, b, pi)
+    model, plan = hmm.Model(a, b, pi), hmm.Plan(off)
+    d_obs = torch.from_numpy(obs.astype(np.int16)).cuda()
+    ll, path = hmm.forward_viterbi_device(model, plan, d_obs)
+    ll, path = ll.cpu().numpy(), path.cpu().numpy()
+    _check_all_blocks(t, obs, off, ll, path)
+    assert np.array_equal(hmm.viterbi_device(model, plan, d_obs).cpu().numpy(), path)
+    plan.reserve(27, posterior=True)
+    post = hmm.posterior_device(model, plan, d_obs)
+    assert float((post.sum(dim=1) - 1.0).abs().max()) < 1e-12
+    assert _posterior_every_block(t, obs, off, post) == 10_000_000
+    del post, d_obs
+    torch.cuda.empty_cache()

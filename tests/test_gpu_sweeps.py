@@ -55,7 +55,7 @@ def test_golden_sweeps(gpu, name):
     np.testing.assert_allclose(post[g["post_rows"]], g["post"], rtol=RTOL, atol=1e-300)
 
 
-@pytest.mark.parametrize("n", [1, 4, 16, 17, 27, 64, 65, 70, 72, 96, 133, 150, 192])
+@pytest.mark.parametrize("n", [1, 4, 16, 17, 27, 64, 65, 70, 72, 96, 133, 137, 141, 144, 150, 192])
 def test_random_vs_oracle(gpu, n):
     rng = np.random.default_rng(1000 + n)
     a, b, pi = random_hmm(rng, n)
@@ -328,3 +328,19 @@ def test_wrappers_host_blocks_paths(gpu):
     ll = hmm.loglik_wrapper(a, b, pi, sub)
     ref = O.forward_loglik(build_tables(a, b, pi), so, soff)
     assert abs(ll - (ref[0] + ref[1])) <= 1e-9 * abs(ll)
+
+
+@pytest.mark.parametrize("n", [133, 141, 144])
+def test_single_long_block_vs_oracle(gpu, n):
+    """One block only: the forward sweep has no matrix-core group (every task is a VALU
+    half of the split block), the Viterbi runs the lane-group layout alone, and at
+    N = 137..144 both must cover every source state (sources 136..143 were outside the
+    previous VALU configurations' lanes)."""
+    rng = np.random.default_rng(77 + n)
+    a, b, pi = random_hmm(rng, n)
+    obs, off, _ = sample_alignment(a, b, pi, [5000], seed=n, p_n=0.03, p_gap=0.02)
+    t = build_tables(a, b, pi)
+    ll, path, post = run_all(a, b, pi, obs, off)
+    np.testing.assert_allclose(ll, O.forward_loglik(t, obs, off), rtol=RTOL, atol=0)
+    np.testing.assert_array_equal(path, O.viterbi(t, obs, off))
+    np.testing.assert_allclose(post, O.posterior(t, obs, off), rtol=RTOL, atol=1e-300)
