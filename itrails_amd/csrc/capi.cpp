@@ -213,8 +213,11 @@ int vit_stride(int n) {
 }
 
 // matrix-core posterior exists: 100 blocks of 100 kbp at N = 70, 51.3 against 61.4 ms)
+// Small models (N <= 48) are latency-bound at any block count: the whole posterior's work is
+// a fraction of the longest block's two sweeps (the reference's example (3,3) model, N = 27,
+// 10 Mbp: ~1 ms of VALU work against 18,377 x (~0.2 + ~0.4) us), so they take the split too.
 bool post_split_path(int n, itr_plan_t p) {
-  return p->npsplit > 0 && n <= 128 && p->nblocks <= 2 * (int64_t)cu_count();
+  return p->npsplit > 0 && n <= 128 && (p->nblocks <= 2 * (int64_t)cu_count() || n <= 48);
 }
 
 // posterior (matrix-core form): blocks at least this fraction of the longest get their
@@ -343,7 +346,8 @@ constexpr int64_t kCombCols = 256;  // columns per combine task of the posterior
 int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const itr::MfmaGeometry& g,
                hipStream_t st, const char* tname, bool valu = true, bool mfma = true,
                int64_t max_grid = -1, bool zero_queues = true, int cus = 0,
-               bool share_cu = false, int64_t nbeta = 0, int qbase = 3) {
+               bool share_cu = false, int64_t nbeta = 0, int qbase = 3,
+               bool valu_fwd = true) {
   if (cus <= 0) cus = cu_count();
   itr::MfmaArgs a{};
   a.n = m->n;
@@ -353,7 +357,7 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
     const double lim = std::max(512.0, g.pfrac * (double)(p->nblocks ? p->sorted_len[0] : 0));
     while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
     v.order = p->d_order;
-    v.nblocks = nurg;
+    v.nblocks = valu_fwd ? nurg : 0;  // (false: the beta tasks only; nurg still sets the groups)
     v.nbeta = mode == itr::MODE_FWD_STORE ? nbeta : 0;
   }
   a.ngroups = ll ? p->ngroups_ll : (p->nblocks - nurg + 3) / 4;
@@ -828,7 +832,12 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
   // Few blocks, all long (e.g. 100 blocks of 100 kbp): one CU per block for the 9-wave
   // Viterbi sweep and the forward sweep beside it on the remaining CUs (at least a quarter
   // of the chip), instead of one after the other
-  const bool few = !wave && fwd_loglik && p->nblocks <= cus - cus / 4;
+  // Small models (N <= 48, e.g. the reference's example (3,3) model, N = 27): both sweeps
+  // are bound by the longest block's step latency, not by throughput (10 Mbp at N = 27:
+  // Viterbi 3.6 ms = 18,377 x 195 ns, forward 2.0 ms), so they run side by side on two halves
+  // of the chip instead of one after the other
+  const bool small = !wave && fwd_loglik && m->n <= 48;
+  const bool few = !wave && fwd_loglik && (p->nblocks <= cus - cus / 4 || small);
   if (few) {
     // the Viterbi blocks alone on their CUs (masked), the forward on the others with as
     // many workgroups per CU as it needs to run every task at once (100 x 100 kbp: 200
@@ -838,7 +847,8 @@ int viterbi_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, uint8_t* path
     // one CU per block in whole shader-engine sets (32 CUs: one per engine of every XCC):
     // the dispatcher deals the blocks' workgroups to the engines in turn
     const int X = (cus % 32 == 0) ? 32 : 1;
-    const int rv = (int)std::min<int64_t>((p->nblocks + X - 1) / X * X, cus - cus / 4);
+    const int rv = small ? (cus / 2 + X - 1) / X * X
+                         : (int)std::min<int64_t>((p->nblocks + X - 1) / X * X, cus - cus / 4);
     if (int e = partition(rv, 0, &pt)) return e;
     HIP_TRY(hipEventRecord(pt->fork, st));
     HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
@@ -1192,12 +1202,72 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
       a.beta_off = p->d_boff;
       a.sub_lo = p->d_sublo;
     }
-    // the two launches' work counters ([3, 4] forward, [5, 6] backward) and the combine
-    // tasks' ([7]) zeroed by one memset up front
+    // the two launches' work counters ([3, 4] forward, [5, 6] backward), the combine
+    // tasks' ([7]) and the split forward launch's beta tasks' ([14]) zeroed up front
     HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 5 * sizeof(int), st));
-    if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, st, "posterior_fwd", true, true, -1,
-                           false, 0, false, nbeta))
+    HIP_TRY(hipMemsetAsync(p->d_queue + 14, 0, sizeof(int), st));
+    const itr::FwdGroupGeometry fgeo = itr::fwd_group_geometry(m->n);
+    const int64_t nurg = [&] {
+      const double lim = std::max(512.0, g.pfrac * (double)p->sorted_len[0]);
+      int64_t k = 0;
+      while (k < p->nblocks && (double)p->sorted_len[k] > lim) ++k;
+      return k;
+    }();
+    bool part = nurg > 0 && fgeo.block > 0 && fgeo.xr == g.xr;
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_NO_FWD_GROUPS")) part = false;
+#endif
+    if (part) {
+      // The longest blocks' forward sweeps (the launch's critical path) one per reserved CU on
+      // the lane-group layout (lng2), their beta sweeps one per CU of a second reserved set
+      // (lng), the matrix-core groups on the rest; both sets join the groups when done
+      const int ncu = cu_count();
+      const int X = (ncu % 8 == 0) ? 8 : 1;
+      const int rf = (int)std::min<int64_t>((nurg + X - 1) / X * X, ncu / 4);
+      const int rb = nbeta > 0 ? (int)std::min<int64_t>((nbeta + X - 1) / X * X, ncu / 4) : 0;
+      Partition* pt = nullptr;
+      if (int e = partition(rb, rf, &pt)) return e;
+      Scope sc("posterior_fwd", st);
+      HIP_TRY(hipEventRecord(pt->fork, st));
+      HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
+      HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
+      HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
+      const int ocus = ncu - rf - rb;
+      if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, pt->blk, nullptr, false, true,
+                             (int64_t)g.per_cu * ocus, false, ocus))
+        return e;
+      {
+        itr::SweepArgs v = a;
+        v.order = p->d_order;
+        v.nblocks = nurg;
+        v.queue = p->d_queue + 3;
+        v.prio_len = 0;
+        itr::FwdGroupGeometry gx = fgeo;
+        gx.lds = std::max(gx.lds, itr::kExclusiveLds);  // one per CU
+        HIP_TRY(itr::launch_fwd_group(gx, (int)std::min<int64_t>(rf, nurg), v, pt->lng2,
+                                      itr::MODE_FWD_STORE));
+      }
+      if (rb > 0 &&
+          (run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, pt->lng, nullptr, true, false, rb, false,
+                      rb, false, nbeta, 14, false) != 0))
+        return ITR_EHIP;
+      if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, pt->lng2, nullptr, false, true,
+                             (int64_t)g.per_cu * rf, false, rf))
+        return e;
+      if (rb > 0)
+        if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, pt->lng, nullptr, false, true,
+                               (int64_t)g.per_cu * rb, false, rb))
+          return e;
+      HIP_TRY(hipEventRecord(pt->jl, pt->lng));
+      HIP_TRY(hipEventRecord(pt->jl2, pt->lng2));
+      HIP_TRY(hipEventRecord(pt->jb, pt->blk));
+      HIP_TRY(hipStreamWaitEvent(st, pt->jl, 0));
+      HIP_TRY(hipStreamWaitEvent(st, pt->jl2, 0));
+      HIP_TRY(hipStreamWaitEvent(st, pt->jb, 0));
+    } else if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, st, "posterior_fwd", true,
+                                  true, -1, false, 0, false, nbeta)) {
       return e;
+    }
     a.post = post;
     a.beta = nullptr;
     a.beta_in = nbeta > 0 ? p->d_beta : nullptr;

@@ -65,10 +65,10 @@ __global__ void __launch_bounds__(64 * W, ((W + 3) / 4 > 2 ? (W + 3) / 4 : 2))
     vit_group_kernel(SweepArgs p) {
   vit_group_device<G, W, S>(p);
 }
-template <int G, int W, int S>
+template <int G, int W, int S, int MODE>
 __global__ void __launch_bounds__(64 * W, ((W + 3) / 4 > 2 ? (W + 3) / 4 : 2))
     fwd_group_kernel(SweepArgs p) {
-  fwd_group_device<G, W, S>(p);
+  fwd_group_device<G, W, S, MODE>(p);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -113,7 +113,9 @@ static constexpr Cfg kCfgs[] = {
     // (N <= 72), five lanes per target and 12 targets per wave (N <= 140 / 150)
     {-3, 4, 1, 24}, {-5, 12, 1, 28}, {-5, 12, 1, 30},
     // eight lanes per target, three targets per lane, six waves, 144 sources (N <= 144)
-    {8, 6, 3, 18}};
+    {8, 6, 3, 18},
+    // Viterbi only, lane groups of three, two waves (N <= 30)
+    {-3, 2, 1, 10}};
 static constexpr int kNarrow = 7;  // entries 0..6
 [[maybe_unused]] static constexpr int kNumCfgs = (int)(sizeof kCfgs / sizeof kCfgs[0]);
 
@@ -218,6 +220,7 @@ static hipError_t dispatch(int cfg, bool launch, const SweepArgs* a, int grid, s
       case 22: return dispatch_group<3, 4, 24>(launch, a, grid, lds, st, occ);
       case 23: return dispatch_group<5, 12, 28>(launch, a, grid, lds, st, occ);
       case 24: return dispatch_group<5, 12, 30>(launch, a, grid, lds, st, occ);
+      case 26: return dispatch_group<3, 2, 10>(launch, a, grid, lds, st, occ);
     }
   }
 #define ITR_CFG(C, QL, WV, RJN, IQ)                                          \
@@ -297,17 +300,24 @@ FwdGroupGeometry fwd_group_geometry(int n) {
   g.xr = L::XR;
   g.lds = L::lds_bytes;
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fwd_group_kernel<3, 4, 24>, L::TB,
-                                                   g.lds) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fwd_group_kernel<3, 4, 24, MODE_FWD_LL>,
+                                                   L::TB, g.lds) != hipSuccess)
     nb = 1;
   g.per_cu = nb > 0 ? nb : 1;
   return g;
 }
 
 hipError_t launch_fwd_group(const FwdGroupGeometry& g, int grid, const SweepArgs& a,
-                            hipStream_t st) {
+                            hipStream_t st, int mode) {
   if (g.block != 256 || grid <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((fwd_group_kernel<3, 4, 24>), dim3(grid), dim3(g.block), g.lds, st, a);
+  if (mode == MODE_FWD_LL)
+    hipLaunchKernelGGL((fwd_group_kernel<3, 4, 24, MODE_FWD_LL>), dim3(grid), dim3(g.block), g.lds,
+                       st, a);
+  else if (mode == MODE_FWD_STORE)
+    hipLaunchKernelGGL((fwd_group_kernel<3, 4, 24, MODE_FWD_STORE>), dim3(grid), dim3(g.block),
+                       g.lds, st, a);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

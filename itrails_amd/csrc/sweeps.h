@@ -277,8 +277,9 @@ struct FwdGroupGeometry {
   int per_cu;   // resident workgroups per CU
 };
 FwdGroupGeometry fwd_group_geometry(int n);
+// mode: MODE_FWD_LL (a.tasks) or MODE_FWD_STORE (a.order: the posterior's forward rows)
 hipError_t launch_fwd_group(const FwdGroupGeometry& g, int grid, const SweepArgs& a,
-                            hipStream_t st);
+                            hipStream_t st, int mode = MODE_FWD_LL);
 
 // log-likelihoods of the split blocks of a forward sweep
 hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,
