@@ -235,7 +235,11 @@ std::pair<int64_t, int64_t> hybrid_beta_set(itr_plan_t p, int n) {
   int64_t nurg = 0, nbeta = 0, brows = 0;
   const double lim = std::max(512.0, gb.pfrac * (double)p->sorted_len[0]);
   while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
-  const double blim = std::max(512.0, kPostBetaFrac * (double)p->sorted_len[0]);
+  double bfrac = kPostBetaFrac;
+#ifdef ITR_EXPERIMENT
+  if (getenv("ITR_POST_BFRAC")) bfrac = atof(getenv("ITR_POST_BFRAC"));
+#endif
+  const double blim = std::max(512.0, bfrac * (double)p->sorted_len[0]);
   while (nbeta < std::min(p->npsplit, nurg) && (double)p->sorted_len[nbeta] >= blim)
     brows += p->sorted_len[nbeta++];
   return {nbeta, brows};
@@ -346,8 +350,7 @@ constexpr int64_t kCombCols = 256;  // columns per combine task of the posterior
 int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const itr::MfmaGeometry& g,
                hipStream_t st, const char* tname, bool valu = true, bool mfma = true,
                int64_t max_grid = -1, bool zero_queues = true, int cus = 0,
-               bool share_cu = false, int64_t nbeta = 0, int qbase = 3,
-               bool valu_fwd = true) {
+               bool share_cu = false, int64_t nbeta = 0, int qbase = 3) {
   if (cus <= 0) cus = cu_count();
   itr::MfmaArgs a{};
   a.n = m->n;
@@ -357,7 +360,7 @@ int run_hybrid(int mode, itr_model_t m, itr_plan_t p, itr::SweepArgs v, const it
     const double lim = std::max(512.0, g.pfrac * (double)(p->nblocks ? p->sorted_len[0] : 0));
     while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
     v.order = p->d_order;
-    v.nblocks = valu_fwd ? nurg : 0;  // (false: the beta tasks only; nurg still sets the groups)
+    v.nblocks = nurg;
     v.nbeta = mode == itr::MODE_FWD_STORE ? nbeta : 0;
   }
   a.ngroups = ll ? p->ngroups_ll : (p->nblocks - nurg + 3) / 4;
@@ -1166,7 +1169,10 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
     // matrix-core bulk of the backward launch.  (Splitting the forward sweep as well — a
     // forward + posterior sweep over [hi, T) in the backward launch — measured slower: 24.1
     // against 23.0 ms per (7,7) posterior, profiles/r5ps3_*.)
-    const double lofrac = kPostBetaLo;
+    double lofrac = kPostBetaLo;
+#ifdef ITR_EXPERIMENT
+    if (getenv("ITR_POST_LO")) lofrac = atof(getenv("ITR_POST_LO"));
+#endif
     // (split blocks are VALU tasks of the backward launch: a prefix of its VALU set, whose
     // limit mirrors run_hybrid's; their forward sweep is a VALU task or a matrix-core group)
     const auto [nbeta, brows] = hybrid_beta_set(p, m->n);
@@ -1202,72 +1208,16 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
       a.beta_off = p->d_boff;
       a.sub_lo = p->d_sublo;
     }
-    // the two launches' work counters ([3, 4] forward, [5, 6] backward), the combine
-    // tasks' ([7]) and the split forward launch's beta tasks' ([14]) zeroed up front
+    // the two launches' work counters ([3, 4] forward, [5, 6] backward) and the combine
+    // tasks' ([7]) zeroed by one memset up front
     HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 5 * sizeof(int), st));
-    HIP_TRY(hipMemsetAsync(p->d_queue + 14, 0, sizeof(int), st));
-    const itr::FwdGroupGeometry fgeo = itr::fwd_group_geometry(m->n);
-    const int64_t nurg = [&] {
-      const double lim = std::max(512.0, g.pfrac * (double)p->sorted_len[0]);
-      int64_t k = 0;
-      while (k < p->nblocks && (double)p->sorted_len[k] > lim) ++k;
-      return k;
-    }();
-    bool part = nurg > 0 && fgeo.block > 0 && fgeo.xr == g.xr;
-#ifdef ITR_EXPERIMENT
-    if (getenv("ITR_NO_FWD_GROUPS")) part = false;
-#endif
-    if (part) {
-      // The longest blocks' forward sweeps (the launch's critical path) one per reserved CU on
-      // the lane-group layout (lng2), their beta sweeps one per CU of a second reserved set
-      // (lng), the matrix-core groups on the rest; both sets join the groups when done
-      const int ncu = cu_count();
-      const int X = (ncu % 8 == 0) ? 8 : 1;
-      const int rf = (int)std::min<int64_t>((nurg + X - 1) / X * X, ncu / 4);
-      const int rb = nbeta > 0 ? (int)std::min<int64_t>((nbeta + X - 1) / X * X, ncu / 4) : 0;
-      Partition* pt = nullptr;
-      if (int e = partition(rb, rf, &pt)) return e;
-      Scope sc("posterior_fwd", st);
-      HIP_TRY(hipEventRecord(pt->fork, st));
-      HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
-      HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
-      HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
-      const int ocus = ncu - rf - rb;
-      if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, pt->blk, nullptr, false, true,
-                             (int64_t)g.per_cu * ocus, false, ocus))
-        return e;
-      {
-        itr::SweepArgs v = a;
-        v.order = p->d_order;
-        v.nblocks = nurg;
-        v.queue = p->d_queue + 3;
-        v.prio_len = 0;
-        itr::FwdGroupGeometry gx = fgeo;
-        gx.lds = std::max(gx.lds, itr::kExclusiveLds);  // one per CU
-        HIP_TRY(itr::launch_fwd_group(gx, (int)std::min<int64_t>(rf, nurg), v, pt->lng2,
-                                      itr::MODE_FWD_STORE));
-      }
-      if (rb > 0 &&
-          (run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, pt->lng, nullptr, true, false, rb, false,
-                      rb, false, nbeta, 14, false) != 0))
-        return ITR_EHIP;
-      if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, pt->lng2, nullptr, false, true,
-                             (int64_t)g.per_cu * rf, false, rf))
-        return e;
-      if (rb > 0)
-        if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, pt->lng, nullptr, false, true,
-                               (int64_t)g.per_cu * rb, false, rb))
-          return e;
-      HIP_TRY(hipEventRecord(pt->jl, pt->lng));
-      HIP_TRY(hipEventRecord(pt->jl2, pt->lng2));
-      HIP_TRY(hipEventRecord(pt->jb, pt->blk));
-      HIP_TRY(hipStreamWaitEvent(st, pt->jl, 0));
-      HIP_TRY(hipStreamWaitEvent(st, pt->jl2, 0));
-      HIP_TRY(hipStreamWaitEvent(st, pt->jb, 0));
-    } else if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, st, "posterior_fwd", true,
-                                  true, -1, false, 0, false, nbeta)) {
+    // (the longest blocks' forward sweeps on lane groups, one per reserved CU beside the
+    // matrix-core groups on the others, measured slower: 18.2 against 15.2 ms per (5,5)
+    // posterior — the groups lost 80 CUs for most of the launch, profiles/r6d_posterior_ab.txt;
+    // in one launch a VALU task and a group workgroup share each CU)
+    if (int e = run_hybrid(itr::MODE_FWD_STORE, m, p, a, g, st, "posterior_fwd", true, true, -1,
+                           false, 0, false, nbeta))
       return e;
-    }
     a.post = post;
     a.beta = nullptr;
     a.beta_in = nbeta > 0 ? p->d_beta : nullptr;

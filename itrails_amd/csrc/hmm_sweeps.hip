@@ -310,14 +310,9 @@ FwdGroupGeometry fwd_group_geometry(int n) {
 hipError_t launch_fwd_group(const FwdGroupGeometry& g, int grid, const SweepArgs& a,
                             hipStream_t st, int mode) {
   if (g.block != 256 || grid <= 0) return hipErrorInvalidValue;
-  if (mode == MODE_FWD_LL)
-    hipLaunchKernelGGL((fwd_group_kernel<3, 4, 24, MODE_FWD_LL>), dim3(grid), dim3(g.block), g.lds,
-                       st, a);
-  else if (mode == MODE_FWD_STORE)
-    hipLaunchKernelGGL((fwd_group_kernel<3, 4, 24, MODE_FWD_STORE>), dim3(grid), dim3(g.block),
-                       g.lds, st, a);
-  else
-    return hipErrorInvalidValue;
+  if (mode != MODE_FWD_LL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((fwd_group_kernel<3, 4, 24, MODE_FWD_LL>), dim3(grid), dim3(g.block), g.lds,
+                     st, a);
   return hipGetLastError();
 }
 
