@@ -188,6 +188,7 @@ def pmc_traffic(n, mode, tag_hint=""):
             parts = [(k, v) for k, v in d.items() if isinstance(v, dict) and
                      v.get("n_states", 70) == n and
                      "hbm_bytes_raw" in v and ("wave_vit_kernel" in k or
+                                               "vit_group_kernel<" in k or
                                                (k.startswith("void itr::sweep_kernel<") and
                                                 k.endswith(", 3>(itr::SweepArgs)")))]
             if len(parts) == 2:
@@ -201,6 +202,23 @@ def pmc_traffic(n, mode, tag_hint=""):
                     f"{os.path.basename(f)} (" + " + ".join(k for k, _ in parts) +
                     "): 2 x FETCH_SIZE + WRITE_SIZE per call (all launches of each kernel; "
                     "gfx950 FETCH correction)")
+        if mode == 2:  # posterior: both launches of the step (forward-store + backward)
+            def mode_of(name):
+                h = re.search(r"hybrid_sweep_kernel<\d+, \d+, \d+, (\d+),", name)
+                if h:
+                    return int(h.group(1))
+                m = re.search(r"sweep_kernel<[^>]*, (\d+)>\(itr::SweepArgs\)$", name)
+                return int(m.group(1)) if m else -1
+            parts = [(k, v) for k, v in d.items() if isinstance(v, dict) and
+                     v.get("n_states", 70) == n and "hbm_bytes_raw" in v and
+                     mode_of(k) in (1, 2)]
+            if {mode_of(k) for k, _ in parts} == {1, 2}:
+                return round(sum(v.get("hbm_bytes_fetch_x2", v["hbm_bytes_raw"])
+                                 for _, v in parts)), (
+                    f"{os.path.basename(f)} (" + " + ".join(k for k, _ in parts) +
+                    "): 2 x FETCH_SIZE + WRITE_SIZE per launch, both launches of the step "
+                    "(gfx950 FETCH correction)")
+            continue
         for name, v in d.items():
             if not isinstance(v, dict):
                 continue

@@ -2,8 +2,8 @@
 default bench command (scripts/r4/final.sh: rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE,
 over `bench.py --steps 3 --warmup 1 --verify 0`): every launch of the call's kernels — the
 mixed launch and the two reserved sets' late launches (wave_mixed_kernel, roles 0/1/2), the
-long blocks' Viterbi sweep (sweep_kernel<VIT>) and the forward's VALU halves
-(hybrid_sweep_kernel<FWD_LL>) — divided by the number of calls (one role-0 mixed launch per
+long blocks' Viterbi sweep (vit_group_kernel; sweep_kernel<VIT> before round 6) and the
+forward's VALU halves (fwd_group_kernel; hybrid_sweep_kernel<FWD_LL> before) — divided by the number of calls (one role-0 mixed launch per
 call).  The two non-mixed kernels also run in the bench's separate forward / Viterbi timing
 calls, so they are counted at their per-dispatch average, once per call.  Units: the
 counters report KiB (MI355X_MICROARCH.md); raw, no gfx950 FETCH correction applied.
@@ -40,7 +40,8 @@ def main(prof, out):
             if "wave_mixed_kernel" in k:
                 per = v * 1024 / calls
             elif ("sweep_kernel<" in k and k.endswith(", 3>(itr::SweepArgs)")) or \
-                    ("hybrid_sweep_kernel<" in k and ", 0, 2," in k):
+                    ("hybrid_sweep_kernel<" in k and ", 0, 2," in k) or \
+                    "vit_group_kernel<" in k or "fwd_group_kernel<" in k:
                 per = v * 1024 / disp[k]
             else:
                 continue
