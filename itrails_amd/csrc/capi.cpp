@@ -220,13 +220,8 @@ bool post_split_path(int n, itr_plan_t p) {
   return p->npsplit > 0 && n <= 128 && (p->nblocks <= 2 * (int64_t)cu_count() || n <= 48);
 }
 
-// posterior (matrix-core form): blocks at least this fraction of the longest get their
-// backward sweep beside their forward one (itr_posterior)
-constexpr double kPostBetaFrac = 0.5;
-constexpr double kPostBetaLo = 0.4;  // their split column, as a fraction of their length
-
 // The matrix-core posterior's split set: the first nbeta blocks of the order (VALU tasks of
-// the backward launch, at least kPostBetaFrac of the longest block and >= 512 columns) and
+// the backward launch, at least MfmaGeometry.bfrac of the longest block and >= 512 columns) and
 // their beta rows (brows = their columns).  itr_posterior splits them, reserve() sizes their
 // rows with it.
 std::pair<int64_t, int64_t> hybrid_beta_set(itr_plan_t p, int n) {
@@ -235,7 +230,7 @@ std::pair<int64_t, int64_t> hybrid_beta_set(itr_plan_t p, int n) {
   int64_t nurg = 0, nbeta = 0, brows = 0;
   const double lim = std::max(512.0, gb.pfrac * (double)p->sorted_len[0]);
   while (nurg < p->nblocks && (double)p->sorted_len[nurg] > lim) ++nurg;
-  double bfrac = kPostBetaFrac;
+  double bfrac = gb.bfrac;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_POST_BFRAC")) bfrac = atof(getenv("ITR_POST_BFRAC"));
 #endif
@@ -1161,15 +1156,15 @@ int itr_posterior(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* post
   if (g.cfg >= 0 && !post_split_path(m->n, p)) {
     // forward rows at the hybrid's stride g.xr for every block (reserve() sized for it)
     const itr::MfmaGeometry gb = itr::mfma_geometry(m->n, itr::MODE_BWD);
-    // The longest blocks (at least kPostBetaFrac of the longest) are split at column
-    // lo = kPostBetaLo x T: their backward sweep over [lo, T) (beta rows) runs beside their
+    // The longest blocks (at least g.bfrac of the longest) are split at column
+    // lo = g.lofrac x T: their backward sweep over [lo, T) (beta rows) runs beside their
     // forward sweep in the forward launch, the backward launch's VALU task sweeps [0, lo]
     // from the stored beta_lo, and post_combine forms the posteriors of (lo, T).  A whole
     // VALU backward + posterior sweep (~0.95 us per column at N = 133) outlasts the
     // matrix-core bulk of the backward launch.  (Splitting the forward sweep as well — a
     // forward + posterior sweep over [hi, T) in the backward launch — measured slower: 24.1
     // against 23.0 ms per (7,7) posterior, profiles/r5ps3_*.)
-    double lofrac = kPostBetaLo;
+    double lofrac = g.lofrac;
 #ifdef ITR_EXPERIMENT
     if (getenv("ITR_POST_LO")) lofrac = atof(getenv("ITR_POST_LO"));
 #endif

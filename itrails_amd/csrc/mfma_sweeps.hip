@@ -591,6 +591,8 @@ struct MCfg {
   int nmin, nmax, nt, nk, gb, viq;  // viq: sources per lane of the VALU tasks (8 lanes)
   double pfrac;  // posterior: blocks longer than pfrac x the longest run as VALU tasks
   bool post;     // the hybrid posterior beats the VALU-only one at this size
+  double bfrac;  // posterior: VALU blocks at least bfrac x the longest are split ...
+  double lofrac; // ... at column lofrac x T (itr_posterior)
 };
 // pfrac measured on the (7,7) model, 10 Mbp (round 2: 0.2 / 0.35 / 0.5 / 0.7 -> 203 / 264 /
 // 281 / 259 M columns/s; round 5, with the long blocks' backward split (itr_posterior):
@@ -600,13 +602,18 @@ struct MCfg {
 // three-wave sweeps in round 2; with round 5's backward step and split, 668-685 against
 // 521-523 M (profiles/r5ab55*): the hybrid serves N = 65..72.  The introgression (5,5)
 // model, N = 95: 421 against 461 M, so 81..96 stays VALU-only; other sizes unmeasured.)
+// bfrac / lofrac: round 5 at N = 133 (0.5 / 0.4, profiles/r5ps_posterior_split.txt; 0.35 /
+// 0.4 / 0.5 within 0.05 ms in round 6).  N = 70 re-swept in round 6 (profiles/r6e_*, r6f_
+// posterior_params.txt): (pfrac, bfrac) = (0.35, 0.5) 14.6-14.8 ms, (0.35, 0.35) 13.2,
+// (0.25, 0.35) 13.0-13.2, (0.2, 0.35) 14.2, (0.3, 0.3) 12.9-13.0, (0.25, 0.3) 12.5-12.7,
+// (0.25, 0.25) 12.4-12.6; lofrac 0.3 / 0.35 / 0.45 / 0.5 no better than 0.4
 constexpr MCfg kMCfgs[] = {
-    {33, 48, 3, 12, 1, 6, 0.35, false},   {49, 64, 4, 16, 1, 8, 0.35, false},
-    {65, 72, 5, 18, 1, 9, 0.35, true},    {73, 80, 5, 20, 1, 10, 0.35, false},
-    {81, 96, 6, 24, 1, 12, 0.35, false},  {129, 136, 9, 34, 1, 17, 0.55, true},
-    {137, 144, 9, 36, 1, 18, 0.55, true},
+    {33, 48, 3, 12, 1, 6, 0.35, false, 0.5, 0.4},   {49, 64, 4, 16, 1, 8, 0.35, false, 0.5, 0.4},
+    {65, 72, 5, 18, 1, 9, 0.25, true, 0.25, 0.4},    {73, 80, 5, 20, 1, 10, 0.35, false, 0.5, 0.4},
+    {81, 96, 6, 24, 1, 12, 0.35, false, 0.5, 0.4},  {129, 136, 9, 34, 1, 17, 0.55, true, 0.5, 0.4},
+    {137, 144, 9, 36, 1, 18, 0.55, true, 0.5, 0.4},
     // two groups per workgroup (experiment configuration, ITR_MCFG)
-    {129, 136, 9, 34, 2, 17, 0.55, true}};
+    {129, 136, 9, 34, 2, 17, 0.55, true, 0.5, 0.4}};
 constexpr int kMCfgsAuto = 7;  // entries picked by state count
 
 template <int NT, int NK, int GB, int MODE, int VIQ>
@@ -694,6 +701,8 @@ MfmaGeometry mfma_geometry(int n, int mode) {
   g.xr = 16 * kMCfgs[g.cfg].nt;
   g.gb = kMCfgs[g.cfg].gb;
   g.pfrac = kMCfgs[g.cfg].pfrac;
+  g.bfrac = kMCfgs[g.cfg].bfrac;
+  g.lofrac = kMCfgs[g.cfg].lofrac;
 #ifdef ITR_EXPERIMENT
   if (getenv("ITR_POST_URGENT_FRAC")) g.pfrac = atof(getenv("ITR_POST_URGENT_FRAC"));
 #endif

@@ -128,6 +128,8 @@ struct MfmaGeometry {
   int gb;       // groups per workgroup
   int per_cu;   // resident workgroups per CU (occupancy API)
   double pfrac; // posterior sweeps: blocks longer than pfrac x the longest are VALU tasks
+  double bfrac; // posterior: VALU-task blocks at least bfrac x the longest are split at ...
+  double lofrac;//   ... column lofrac x T (backward over [lo, T) beside the forward sweep)
   size_t lds_min;  // launch with at least this much LDS (kExclusiveLds: one workgroup per CU)
 };
 

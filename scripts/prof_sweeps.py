@@ -1,7 +1,8 @@
 """Profiling driver (rocprofv3 target): the chr10 workload of bench.py (BASELINE config 2)
 through each sweep entry point separately, so every kernel's counters come from launches of
 one configuration: forward (itr_forward_loglik), Viterbi (itr_viterbi), the combined call
-(itr_forward_viterbi), posterior at --n-int 7.  usage: python scripts/prof_sweeps.py [reps]"""
+(itr_forward_viterbi), posterior at --n-int 7 (post) and 5 (post5).
+usage: python scripts/prof_sweeps.py [reps] [fwd,vit,fv,post,post5]"""
 import os
 import sys
 
@@ -25,6 +26,10 @@ def main():
     ll = torch.empty(plan.nblocks, dtype=torch.float64, device="cuda")
     path = torch.empty(plan.total, dtype=torch.uint8, device="cuda")
     post = None
+    post5 = None
+    if "post5" in which:  # the (5,5) model's posterior over the same 10 Mbp
+        plan.reserve(a.shape[0], posterior=True)
+        post5 = torch.empty((plan.total, a.shape[0]), dtype=torch.float64, device="cuda")
     if "post" in which:  # config 3: the (7,7) model's posterior over the same 10 Mbp
         a7, b7, pi7, _ = load_model(7)
         W7 = make_workload("chr10", a7, b7, pi7, 0, 1, 2000.0)
@@ -34,6 +39,8 @@ def main():
     for _ in range(reps):
         if "post" in which:
             hmm.posterior_device(m7, p7, o7, out=post)
+        if "post5" in which:
+            hmm.posterior_device(model, plan, d_obs, out=post5)
         if "fwd" in which:
             hmm.forward_loglik_device(model, plan, d_obs, out=ll)
         if "vit" in which:
