@@ -257,14 +257,17 @@ __device__ __forceinline__ double wave_max_rows(double v) {
 // from e_{T-1} and ending with a row of ones.  Outputs as the VALU sweep's: the split halves'
 // vectors (row stride XR, the hybrid configuration's, = 16 x its waves) and exponents, or
 // log P = log(sum_j x_j) + K ln 2 (optimizer.py:145-162).
-template <int G, int W, int S, int MODE>
+// XRS: row stride of the stored vectors (split halves, forward rows) when it differs from the
+// layout's slot count (inside the hybrid launch: five waves, the matrix-core layout's 80-wide
+// rows); C: sources per LDS read piece (8 inside the hybrid launch's register budget)
+template <int G, int W, int S, int MODE, int XRS = VitGroupLayout<G, W, S>::XR, int C = 16>
 __device__ __forceinline__ void fwd_group_task(const SweepArgs& p, unsigned char* smem, int bi) {
   static_assert(MODE == MODE_FWD_LL || MODE == MODE_FWD_STORE, "forward modes");
   using Lay = VitGroupLayout<G, W, S>;
   constexpr int GPR = Lay::GPR, TPW = Lay::TPW, XR = Lay::XR, XS = Lay::XS, TE = Lay::TE;
   constexpr int TB = Lay::TB;
   constexpr int NCH = S >= 16 ? 4 : (S >= 6 ? 3 : 2);  // independent FMA chains per lane
-  constexpr int C = 16;
+  static_assert(XRS <= XR, "stored rows within the layout's slots");
   constexpr int NPC = (S + C - 1) / C;
   const int n = p.n;
   const int tid = threadIdx.x;
@@ -278,7 +281,8 @@ __device__ __forceinline__ void fwd_group_task(const SweepArgs& p, unsigned char
   const int j = w * TPW + (l >> 4) * GPR + g;
   const bool jv = lane_ok && j < n;
   const bool owner = jv && q == G - 1;
-  const bool slot_owner = lane_ok && q == G - 1;  // (stores its slot's row entry, 0 if padded)
+  // (stores its slot's row entry, 0 if padded; slots past the stored row stride store nothing)
+  const bool slot_owner = lane_ok && q == G - 1 && j < XRS;
 
   double* X = reinterpret_cast<double*>(smem);  // [2][XS+64] published x + write sinks
   double* RED = X + 2 * (XS + 64);              // [5][64] rescale maxima, loglik partials
@@ -329,7 +333,7 @@ __device__ __forceinline__ void fwd_group_task(const SweepArgs& p, unsigned char
       const int o0 = ot.get(0);
       const double* x0tab = split < 0 ? p.emit : p.init;
       double x = jv ? x0tab[o0 * n + j] : 0.0;
-      if (MODE == MODE_FWD_STORE && slot_owner) p.alpha[c0 * XR + j] = x;
+      if (MODE == MODE_FWD_STORE && slot_owner) p.alpha[c0 * XRS + j] = x;
       int K = 0;  // sum of the power-of-two exponents divided out so far
       wait_vmem_all();
       for (int t0 = 0; t0 < T; t0 += TE) {
@@ -387,14 +391,14 @@ __device__ __forceinline__ void fwd_group_task(const SweepArgs& p, unsigned char
               for (int c = 1; c < NCH; ++c) sum += acc[c];
               x = group_sum_last<G>(sum) * ec;
             }
-            if (MODE == MODE_FWD_STORE && slot_owner) p.alpha[(c0 + t) * XR + j] = jv ? x : 0.0;
+            if (MODE == MODE_FWD_STORE && slot_owner) p.alpha[(c0 + t) * XRS + j] = jv ? x : 0.0;
           }
         }
       }
       if (MODE == MODE_FWD_STORE) {
       } else if (split != 0) {  // half of a split block: the scaled vector and its exponent
         const int side = split < 0;
-        if (owner) p.svec[((int64_t)slot * 2 + side) * XR + j] = x;
+        if (owner) p.svec[((int64_t)slot * 2 + side) * XRS + j] = x;
         if (tid == 0) p.sK[slot * 2 + side] = K;
       } else {  // log P = log(sum_j x_j) + K ln 2
         const double part = wave_sum(owner ? x : 0.0);
