@@ -65,10 +65,10 @@ __global__ void __launch_bounds__(64 * W, ((W + 3) / 4 > 2 ? (W + 3) / 4 : 2))
     vit_group_kernel(SweepArgs p) {
   vit_group_device<G, W, S>(p);
 }
-template <int G, int W, int S, int MODE>
+template <int G, int W, int S>
 __global__ void __launch_bounds__(64 * W, ((W + 3) / 4 > 2 ? (W + 3) / 4 : 2))
     fwd_group_kernel(SweepArgs p) {
-  fwd_group_device<G, W, S, MODE>(p);
+  fwd_group_device<G, W, S>(p);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -300,19 +300,17 @@ FwdGroupGeometry fwd_group_geometry(int n) {
   g.xr = L::XR;
   g.lds = L::lds_bytes;
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fwd_group_kernel<3, 4, 24, MODE_FWD_LL>,
-                                                   L::TB, g.lds) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fwd_group_kernel<3, 4, 24>, L::TB, g.lds) !=
+      hipSuccess)
     nb = 1;
   g.per_cu = nb > 0 ? nb : 1;
   return g;
 }
 
 hipError_t launch_fwd_group(const FwdGroupGeometry& g, int grid, const SweepArgs& a,
-                            hipStream_t st, int mode) {
+                            hipStream_t st) {
   if (g.block != 256 || grid <= 0) return hipErrorInvalidValue;
-  if (mode != MODE_FWD_LL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((fwd_group_kernel<3, 4, 24, MODE_FWD_LL>), dim3(grid), dim3(g.block), g.lds,
-                     st, a);
+  hipLaunchKernelGGL((fwd_group_kernel<3, 4, 24>), dim3(grid), dim3(g.block), g.lds, st, a);
   return hipGetLastError();
 }
 

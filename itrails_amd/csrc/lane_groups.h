@@ -248,26 +248,22 @@ __device__ __forceinline__ double wave_max_rows(double v) {
   return rows4_max(v);
 }
 
-// One forward task on the lane-group layout: MODE_FWD_LL (tasks {block, split, slot} as the
-// VALU sweep's, valu_sweep.h: the longest blocks' halves of the split forward, meet in the
-// middle) or MODE_FWD_STORE (block order[bi], the posterior's rescaled forward rows stored at
-// stride XR, padded states 0), at the lowest step latency.  x_t = (x_{t-1} @ a) * e_t in the
+// One forward log-likelihood task (MODE_FWD_LL, tasks {block, split, slot} as the VALU
+// sweep's, valu_sweep.h) on the lane-group layout: the longest blocks' halves of the split
+// forward (meet in the middle) at the lowest step latency.  x_t = (x_{t-1} @ a) * e_t in the
 // probability domain with an exact power-of-two rescale every 8 columns (the exponents summed
 // in K); a backward half (split < 0) runs the same step on a^T from its block's end, starting
 // from e_{T-1} and ending with a row of ones.  Outputs as the VALU sweep's: the split halves'
-// vectors (row stride XR, the hybrid configuration's, = 16 x its waves) and exponents, or
-// log P = log(sum_j x_j) + K ln 2 (optimizer.py:145-162).
-// XRS: row stride of the stored vectors (split halves, forward rows) when it differs from the
-// layout's slot count (inside the hybrid launch: five waves, the matrix-core layout's 80-wide
-// rows); C: sources per LDS read piece (8 inside the hybrid launch's register budget)
-template <int G, int W, int S, int MODE, int XRS = VitGroupLayout<G, W, S>::XR, int C = 16>
+// vectors (row stride XR, = the hybrid configuration's 16 x its waves) and exponents, or
+// log P = log(sum_j x_j) + K ln 2 (optimizer.py:145-162).  (A forward-store form of this task,
+// the posterior's longest blocks, measured slower in both placements tried: DESIGN.md §0.)
+template <int G, int W, int S>
 __device__ __forceinline__ void fwd_group_task(const SweepArgs& p, unsigned char* smem, int bi) {
-  static_assert(MODE == MODE_FWD_LL || MODE == MODE_FWD_STORE, "forward modes");
   using Lay = VitGroupLayout<G, W, S>;
   constexpr int GPR = Lay::GPR, TPW = Lay::TPW, XR = Lay::XR, XS = Lay::XS, TE = Lay::TE;
   constexpr int TB = Lay::TB;
   constexpr int NCH = S >= 16 ? 4 : (S >= 6 ? 3 : 2);  // independent FMA chains per lane
-  static_assert(XRS <= XR, "stored rows within the layout's slots");
+  constexpr int C = 16;
   constexpr int NPC = (S + C - 1) / C;
   const int n = p.n;
   const int tid = threadIdx.x;
@@ -281,8 +277,6 @@ __device__ __forceinline__ void fwd_group_task(const SweepArgs& p, unsigned char
   const int j = w * TPW + (l >> 4) * GPR + g;
   const bool jv = lane_ok && j < n;
   const bool owner = jv && q == G - 1;
-  // (stores its slot's row entry, 0 if padded; slots past the stored row stride store nothing)
-  const bool slot_owner = lane_ok && q == G - 1 && j < XRS;
 
   double* X = reinterpret_cast<double*>(smem);  // [2][XS+64] published x + write sinks
   double* RED = X + 2 * (XS + 64);              // [5][64] rescale maxima, loglik partials
@@ -297,15 +291,15 @@ __device__ __forceinline__ void fwd_group_task(const SweepArgs& p, unsigned char
 
   RowStage<W, XR, TE> est;
   {
-    const int32_t* td = MODE == MODE_FWD_LL ? p.tasks + 3 * bi : nullptr;
-    const int blk = uni(td ? td[0] : p.order[bi]);
-    const int split = td ? uni(td[1]) : 0;
-    const int slot = td ? uni(td[2]) : 0;
+    const int32_t* td = p.tasks + 3 * bi;
+    const int blk = uni(td[0]);
+    const int split = uni(td[1]);
+    const int slot = uni(td[2]);
     const int64_t c0 = p.off[blk];
     const int Tb = uni((int)(p.off[blk + 1] - c0));
     const int T = split > 0 ? split : (split < 0 ? Tb + split + 1 : Tb);
     if (T <= 0) {  // empty block: log-likelihood of nothing is 0
-      if (MODE == MODE_FWD_LL && tid == 0) p.loglik[blk] = 0.0;
+      if (tid == 0) p.loglik[blk] = 0.0;
     } else {
       const bool urgent = T >= p.prio_len;
       if (urgent) __builtin_amdgcn_s_setprio(2);
@@ -333,7 +327,6 @@ __device__ __forceinline__ void fwd_group_task(const SweepArgs& p, unsigned char
       const int o0 = ot.get(0);
       const double* x0tab = split < 0 ? p.emit : p.init;
       double x = jv ? x0tab[o0 * n + j] : 0.0;
-      if (MODE == MODE_FWD_STORE && slot_owner) p.alpha[c0 * XRS + j] = x;
       int K = 0;  // sum of the power-of-two exponents divided out so far
       wait_vmem_all();
       for (int t0 = 0; t0 < T; t0 += TE) {
@@ -391,14 +384,12 @@ __device__ __forceinline__ void fwd_group_task(const SweepArgs& p, unsigned char
               for (int c = 1; c < NCH; ++c) sum += acc[c];
               x = group_sum_last<G>(sum) * ec;
             }
-            if (MODE == MODE_FWD_STORE && slot_owner) p.alpha[(c0 + t) * XRS + j] = jv ? x : 0.0;
           }
         }
       }
-      if (MODE == MODE_FWD_STORE) {
-      } else if (split != 0) {  // half of a split block: the scaled vector and its exponent
+      if (split != 0) {  // half of a split block: the scaled vector and its exponent
         const int side = split < 0;
-        if (owner) p.svec[((int64_t)slot * 2 + side) * XRS + j] = x;
+        if (owner) p.svec[((int64_t)slot * 2 + side) * XR + j] = x;
         if (tid == 0) p.sK[slot * 2 + side] = K;
       } else {  // log P = log(sum_j x_j) + K ln 2
         const double part = wave_sum(owner ? x : 0.0);
@@ -431,7 +422,7 @@ __device__ __forceinline__ void vit_group_device(const SweepArgs& p) {
     vit_group_task<G, W, S>(p, smem, bi);
   }
 }
-template <int G, int W, int S, int MODE>
+template <int G, int W, int S>
 __device__ __forceinline__ void fwd_group_device(const SweepArgs& p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int qslot;
@@ -441,7 +432,7 @@ __device__ __forceinline__ void fwd_group_device(const SweepArgs& p) {
     const int bi = uni(qslot);
     lds_barrier();
     if (bi >= p.nblocks) break;
-    fwd_group_task<G, W, S, MODE>(p, smem, bi);
+    fwd_group_task<G, W, S>(p, smem, bi);
   }
 }
 

@@ -35,18 +35,9 @@
 
 #include "sweeps.h"
 #include "valu_sweep.h"
-#include "lane_groups.h"
 
 namespace itr {
 namespace {
-
-// the posterior's forward-store VALU tasks on lane groups at N = 65..72 (fwd_store_task); a
-// build with -DITR_NO_FWD_STORE_GROUPS keeps the VALU sweep's task (A/B labs)
-#ifdef ITR_NO_FWD_STORE_GROUPS
-constexpr bool kFwdStoreGroups = false;
-#else
-constexpr bool kFwdStoreGroups = true;
-#endif
 
 // reductions over the 16 lanes of a DPP row (= the 16 targets of one block in one wave):
 // quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror, row_ror:8
@@ -529,17 +520,6 @@ __device__ __forceinline__ void mfma_task(const MfmaArgs& p, unsigned char* smem
 // or half of a split block — per workgroup, lowest step latency) first, then the bulk as
 // matrix-core groups.  One launch, one workgroup shape: no co-residency assumption between
 // kernels is needed for the long blocks to start at once.
-// A posterior forward-store VALU task (the longest blocks): at N = 65..72 (five waves, 80-wide
-// rows) on lane groups of three (lane_groups.h; the fifth wave only keeps the barriers), else
-// the VALU sweep's task
-template <int NT, int VRJ, int VIQ>
-__device__ __forceinline__ void fwd_store_task(const SweepArgs& v, unsigned char* smem, int bi) {
-  if constexpr (NT == 5 && VRJ == 2 && VIQ == 9 && kFwdStoreGroups)
-    fwd_group_task<3, 5, 24, MODE_FWD_STORE, 80, 8>(v, smem, bi);
-  else
-    sweep_task<8, NT, VRJ, VIQ, MODE_FWD_STORE>(v, smem, bi);
-}
-
 template <int NT, int NK, int GB, int MODE, int VRJ, int VIQ>
 __global__ void __launch_bounds__(64 * NT, (MOcc<NT, NK, GB, MODE>::value))
     hybrid_sweep_kernel(MfmaArgs p, SweepArgs v) {
@@ -565,13 +545,11 @@ __global__ void __launch_bounds__(64 * NT, (MOcc<NT, NK, GB, MODE>::value))
     if (bi >= nvalu) break;
     if (MODE == MODE_FWD_STORE && bi < 2 * np) {
       if (bi & 1)
-        fwd_store_task<NT, VRJ, VIQ>(v, smem, bi >> 1);
+        sweep_task<8, NT, VRJ, VIQ, MODE_FWD_STORE>(v, smem, bi >> 1);
       else
         sweep_task<8, NT, VRJ, VIQ, MODE_BETA>(v, smem, bi >> 1);
     } else if (MODE == MODE_FWD_STORE && nb > np) {
       sweep_task<8, NT, VRJ, VIQ, MODE_BETA>(v, smem, bi - np);
-    } else if constexpr (MODE == MODE_FWD_STORE) {
-      fwd_store_task<NT, VRJ, VIQ>(v, smem, bi - np);
     } else {
       sweep_task<8, NT, VRJ, VIQ, MODE>(v, smem, bi - np);
     }
@@ -643,10 +621,7 @@ size_t lds_h() {
   using V = ValuSweep<8, NT, 2, VIQ, MODE>;
   // forward-store launches also run backward (beta) tasks
   using VB = ValuSweep<8, NT, 2, VIQ, MODE == MODE_FWD_STORE ? MODE_BETA : MODE>;
-  // (and at five waves their forward tasks on lane groups)
-  const size_t vg = (MODE == MODE_FWD_STORE && NT == 5) ? VitGroupLayout<3, 5, 24>::lds_bytes : 0;
-  return std::max(std::max(MLds<NT, NK, GB, MODE == MODE_BWD>::bytes, vg),
-                  std::max(V::lds_bytes, VB::lds_bytes));
+  return std::max(MLds<NT, NK, GB, MODE == MODE_BWD>::bytes, std::max(V::lds_bytes, VB::lds_bytes));
 }
 template <int NT, int NK, int GB, int MODE, int VIQ>
 hipError_t launch_h(const MfmaArgs& a, const SweepArgs& v, int grid, size_t lds_min,

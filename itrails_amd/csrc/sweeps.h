@@ -279,10 +279,8 @@ struct FwdGroupGeometry {
   int per_cu;   // resident workgroups per CU
 };
 FwdGroupGeometry fwd_group_geometry(int n);
-// mode: MODE_FWD_LL (a.tasks); the task also has a MODE_FWD_STORE form (the posterior's
-// forward rows), not launched: a partitioned forward-store launch measured slower
 hipError_t launch_fwd_group(const FwdGroupGeometry& g, int grid, const SweepArgs& a,
-                            hipStream_t st, int mode = MODE_FWD_LL);
+                            hipStream_t st);
 
 // log-likelihoods of the split blocks of a forward sweep
 hipError_t launch_fwd_split_combine(int n, int xr, int nsplit, const int32_t* split_blk,
