@@ -179,58 +179,66 @@ def summary_files():
 
 
 def pmc_traffic(n, mode, tag_hint=""):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
-    of this command (scripts/gpu_round.sh -> scripts/summarize_profile.py ->
-    profiles/*_summary.json: FETCH_SIZE + WRITE_SIZE from separate passes, raw)."""
+    """HBM bytes of the timed call from the committed rocprofv3 PMC summary OF THIS BUILD of
+    the library (profiles/r*_summary.json with this library's sha256; scripts/gpu_final.sh ->
+    scripts/pmc_summary.py over scripts/prof_sweeps.py: FETCH_SIZE and WRITE_SIZE from
+    separate passes, per-dispatch averages).  Summaries of other builds are not used: a
+    kernel change makes their bytes stale, and the line then carries null."""
+    h = lib_sha256()
+    mine = []
     for f in summary_files():
+        try:
+            if json.load(open(f)).get("library_sha256") == h:
+                mine.append(f)
+        except (OSError, ValueError):
+            pass
+    if not mine:
+        return None, "no PMC summary of this build of the library under profiles/"
+
+    def fx2(v):
+        return v.get("hbm_bytes_fetch_x2", v["hbm_bytes_raw"])
+
+    for f in mine:
         d = json.load(open(f))
-        if mode == 3:  # Viterbi: the long-block sweep and the per-wave sweep of one call
-            parts = [(k, v) for k, v in d.items() if isinstance(v, dict) and
-                     v.get("n_states", 70) == n and
-                     "hbm_bytes_raw" in v and ("wave_vit_kernel" in k or
-                                               "vit_group_kernel<" in k or
-                                               (k.startswith("void itr::sweep_kernel<") and
-                                                k.endswith(", 3>(itr::SweepArgs)")))]
-            if len(parts) == 2:
-                # the per-wave kernel runs as the bulk launch plus one launch per reserved set
-                # that joins the queue: its per-dispatch average times its launches per call
-                # (the profiled command, scripts/r4/final.sh, makes 3 itr_viterbi calls)
-                def per_call(k, v):
-                    return v.get("hbm_bytes_fetch_x2", v["hbm_bytes_raw"]) * (
-                        max(1, round(v.get("calls", 3) / 3)) if "wave_vit_kernel" in k else 1)
-                return round(sum(per_call(k, v) for k, v in parts)), (
-                    f"{os.path.basename(f)} (" + " + ".join(k for k, _ in parts) +
-                    "): 2 x FETCH_SIZE + WRITE_SIZE per call (all launches of each kernel; "
-                    "gfx950 FETCH correction)")
-        if mode == 2:  # posterior: both launches of the step (forward-store + backward)
-            def mode_of(name):
-                h = re.search(r"hybrid_sweep_kernel<\d+, \d+, \d+, (\d+),", name)
-                if h:
-                    return int(h.group(1))
-                m = re.search(r"sweep_kernel<[^>]*, (\d+)>\(itr::SweepArgs\)$", name)
-                return int(m.group(1)) if m else -1
-            parts = [(k, v) for k, v in d.items() if isinstance(v, dict) and
-                     v.get("n_states", 70) == n and "hbm_bytes_raw" in v and
-                     mode_of(k) in (1, 2)]
-            if {mode_of(k) for k, _ in parts} == {1, 2}:
-                return round(sum(v.get("hbm_bytes_fetch_x2", v["hbm_bytes_raw"])
-                                 for _, v in parts)), (
-                    f"{os.path.basename(f)} (" + " + ".join(k for k, _ in parts) +
-                    "): 2 x FETCH_SIZE + WRITE_SIZE per launch, both launches of the step "
+        items = [(k, v) for k, v in d.items() if isinstance(v, dict) and
+                 v.get("n_states", 70) == n and "hbm_bytes_raw" in v]
+        if mode == 3:  # itr_viterbi: every launch of one call
+            # the per-wave bulk launch and the reserved sets' late launches (roles 0/1/2, one
+            # dispatch each), the long set on both reserved sets (two dispatches), the
+            # traceback of the long set
+            parts = [(k, v, 2 if "vit_group_kernel<" in k else 1) for k, v in items
+                     if "wave_vit_kernel" in k or "vit_group_kernel<" in k or
+                     "vit_trace_kernel" in k]
+            if any("wave_vit_kernel" in k for k, _, _ in parts):
+                return round(sum(fx2(v) * c for _, v, c in parts)), (
+                    f"{os.path.basename(f)} (" + " + ".join(
+                        (f"2 x " if c == 2 else "") + k for k, _, c in parts) +
+                    "): 2 x FETCH_SIZE + WRITE_SIZE per itr_viterbi call, this build "
                     "(gfx950 FETCH correction)")
             continue
-        for name, v in d.items():
-            if not isinstance(v, dict):
-                continue
+        if mode == 2:  # posterior: both launches of the step (forward-store + backward)
+            def mode_of(name):
+                hm = re.search(r"hybrid_sweep_kernel<\d+, \d+, \d+, (\d+),", name)
+                if hm:
+                    return int(hm.group(1))
+                m = re.search(r"sweep_kernel<[^>]*, (\d+)>\(itr::SweepArgs\)$", name)
+                return int(m.group(1)) if m else -1
+            parts = [(k, v) for k, v in items if mode_of(k) in (1, 2)]
+            if {mode_of(k) for k, _ in parts} == {1, 2}:
+                return round(sum(fx2(v) for _, v in parts)), (
+                    f"{os.path.basename(f)} (" + " + ".join(k for k, _ in parts) +
+                    "): 2 x FETCH_SIZE + WRITE_SIZE per launch, both launches of the step, "
+                    "this build (gfx950 FETCH correction)")
+            continue
+        for name, v in items:
             hyb = re.search(r"hybrid_sweep_kernel<\d+, \d+, \d+, (\d+),", name)
-            if ((name.startswith("void itr::sweep_kernel<") and
-                 name.endswith(f", {mode}>(itr::SweepArgs)")) or
-                    (hyb and int(hyb.group(1)) == mode)) and \
-                    v.get("n_states", 70) == n and "hbm_bytes_raw" in v:
-                return round(v.get("hbm_bytes_fetch_x2", v["hbm_bytes_raw"])), (
-                    f"{os.path.basename(f)} ({name}): 2 x FETCH_SIZE + WRITE_SIZE per launch "
-                    "(gfx950 FETCH correction)")
-    return None, "no PMC summary under profiles/ for this kernel"
+            if (name.startswith("void itr::sweep_kernel<") and
+                    name.endswith(f", {mode}>(itr::SweepArgs)")) or \
+                    (hyb and int(hyb.group(1)) == mode):
+                return round(fx2(v)), (
+                    f"{os.path.basename(f)} ({name}): 2 x FETCH_SIZE + WRITE_SIZE per launch, "
+                    "this build (gfx950 FETCH correction)")
+    return None, "this build's PMC summary holds no launch of this configuration"
 
 
 def lib_sha256():
