@@ -744,9 +744,16 @@ def main():
             ideal_ms = ideal(fma_peak, am_peak)
         dom_ops = (2 if args.mode in ("fv", "posterior") else 1) * pair_ops * cols_local
         achieved = dom_ops / (dom_ms * 1e-3) / 1e12 if dom_ms else 0.0
-        default_fv = args.mode == "fv" and n == 70 and not intro and kind == "chr10" and \
-            args.block_len == 0 and args.mbp is None  # (the profiled command's workload)
-        traffic, traffic_note = fv_call_traffic() if default_fv else pmc_traffic(n, dom_mode)
+        # the profiled workloads: the chr10 layout at N = 70 (every entry point) and N = 133
+        # (posterior) — scripts/prof_sweeps.py; other layouts carry no traffic
+        profiled = kind == "chr10" and not intro and args.block_len == 0 and args.mbp is None
+        default_fv = args.mode == "fv" and n == 70 and profiled
+        if default_fv:
+            traffic, traffic_note = fv_call_traffic()
+        elif profiled and args.mode != "fv":
+            traffic, traffic_note = pmc_traffic(n, dom_mode)
+        else:
+            traffic, traffic_note = None, "no PMC profile of this workload under profiles/"
         rates, rates_src = pmc_rates(n)
         cpu = None
         if opt_mode:
