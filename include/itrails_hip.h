@@ -281,6 +281,15 @@ ITR_API int itr_vanloan_job_norms(int n, const double* h_Q, int n_jobs, const do
 ITR_API int itr_solve_batched(int n, int nrhs, int64_t batch, double* d_M, double* d_R,
                               void* stream);
 
+/* d_out_b = d_M_b^-1 for every b (d_M untouched; d_out must not alias it).  n <= 208: one
+ * workgroup per matrix, in-place Gauss-Jordan in registers with partial-pivoting pivots (a
+ * pass without interchanges that checks the diagonal is the column maximum at every step,
+ * and a pivoting pass for the matrices where it is not); larger n: the LU above against the
+ * identity.  Replaces np.linalg.inv of the deepest-interval matrix (deepest_ti.py:256) and
+ * the Pade denominator's inverse in the Van Loan evaluation (expm.py:141-160). */
+ITR_API int itr_inverse_batched(int n, int64_t batch, const double* d_M, double* d_out,
+                                void* stream);
+
 /* C_b = alpha * A_b (m x k) @ B_b (k x n) + beta * C_b, contiguous row-major batches
  * (MFMA f64 16x16x4 tiles).  The contractions of the chain steps (prob @ (mask E mask),
  * run_markov_chain_ABC.py:9-14; deepest_ti.py:256 product with A_last). */

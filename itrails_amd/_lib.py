@@ -63,6 +63,7 @@ _SIGNATURES = {
     "itr_vanloan_paths_ex": ([_I, _P, _I, _P, _I, _P, _I64, _P, _P, _P, _P, _P, _P], _I),
     "itr_vanloan_job_norms": ([_I, _P, _I, _P, _I, _P, _I64, _P, _P, _P, _P], _I),
     "itr_solve_batched": ([_I, _I, _I64, _P, _P, _P], _I),
+    "itr_inverse_batched": ([_I, _I64, _P, _P, _P], _I),
     "itr_gemm_batched": ([_I, _I, _I, _I64, _D, _P, _P, _D, _P, _P], _I),
     "itr_chain_rows": ([_I, _I, _I, _P, _P, _P, _P, _P, _P, _I64, _P, _I64, _P, _P, _I64, _P],
                        _I),

@@ -621,13 +621,42 @@ int forward_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* logli
       HIP_TRY(hipEventRecord(pt->fork, st));
       HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
       HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
-      if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->blk, nullptr, false, true,
-                             (int64_t)g.per_cu * (ncu - rfr), false, ncu - rfr))
-        return e;
-      if (int e = run_valu_forward(m, p, a, g, pt->lng2, rfr, false)) return e;
-      if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->lng2, nullptr, false, true,
-                             (int64_t)g.per_cu * rfr, false, rfr))
-        return e;
+#ifdef ITR_EXPERIMENT
+      // the groups on the per-wave forward (wave_tasks.h fwd_wave_task) instead of the hybrid
+      const itr::WaveMfmaGeometry wf = itr::wave_mfma_geometry(m->n);
+      if (getenv("ITR_WAVE_FWD") && wf.cfg >= 0 && m->EF) {
+        itr::WaveMfmaArgs f{};
+        f.n = m->n;
+        f.ngroups = p->ngroups_ll;
+        f.groups = p->d_groups_ll;
+        f.tasks = p->d_mtasks;
+        f.queue = p->d_queue + 4;
+        f.off = p->d_off;
+        f.obs = obs;
+        f.a = m->a;
+        f.aT = m->aT;
+        f.ef = m->EF;
+        f.emit = m->E;
+        f.init = m->PIE;
+        f.loglik = loglik;
+        f.svec = p->d_svec;
+        f.sstride = g.xr;
+        f.sK = p->d_sK;
+        f.prio_len = INT32_MAX;
+        HIP_TRY(itr::launch_wave_mfma(wf, wf.per_cu * (ncu - rfr), f, pt->blk));
+        if (int e = run_valu_forward(m, p, a, g, pt->lng2, rfr, false)) return e;
+        HIP_TRY(itr::launch_wave_mfma(wf, wf.per_cu * rfr, f, pt->lng2));
+      } else
+#endif
+      {
+        if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->blk, nullptr, false, true,
+                               (int64_t)g.per_cu * (ncu - rfr), false, ncu - rfr))
+          return e;
+        if (int e = run_valu_forward(m, p, a, g, pt->lng2, rfr, false)) return e;
+        if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->lng2, nullptr, false, true,
+                               (int64_t)g.per_cu * rfr, false, rfr))
+          return e;
+      }
       HIP_TRY(hipEventRecord(pt->jl2, pt->lng2));
       HIP_TRY(hipEventRecord(pt->jb, pt->blk));
       HIP_TRY(hipStreamWaitEvent(st, pt->jl2, 0));
@@ -1399,6 +1428,29 @@ int itr_expm_batched_host(int n, int64_t batch, const double* h_A, double* h_out
   HIP_TRY(hipMemcpy(a.p, h_A, bytes, hipMemcpyHostToDevice));
   if (int e = itr_expm_batched(n, batch, (const double*)a.p, (double*)o.p, nullptr)) return e;
   HIP_TRY(hipMemcpy(h_out, o.p, bytes, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int itr_inverse_batched(int n, int64_t batch, const double* M, double* out, void* stream) {
+  if (n < 1 || batch < 0)
+    return fail(ITR_EINVAL, "bad inverse shape n=%d batch=%lld", n, (long long)batch);
+  if (batch == 0) return 0;
+  if (!M || !out) return fail(ITR_EINVAL, "null device pointer");
+  if (M == out) return fail(ITR_EINVAL, "the inverse is not computed in place");
+  hipStream_t st = (hipStream_t)stream;
+  int* piv = nullptr;
+  double* work = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&piv, (size_t)batch * n * sizeof(int), st));
+  if (n > itr::kInverseRegMax &&
+      hipMallocAsync((void**)&work, (size_t)batch * n * n * sizeof(double), st) != hipSuccess) {
+    (void)hipFreeAsync(piv, st);
+    return fail(ITR_EHIP, "inverse workspace allocation failed");
+  }
+  Scope sc("inverse", st);
+  const hipError_t e = itr::inverse_batched(n, batch, M, out, piv, work, st);
+  (void)hipFreeAsync(piv, st);
+  if (work) (void)hipFreeAsync(work, st);
+  if (e != hipSuccess) return fail(ITR_EHIP, "inverse failed: %s", hipGetErrorString(e));
   return 0;
 }
 

@@ -47,6 +47,12 @@ hipError_t group_sum(int64_t nn, int ngroups, const int32_t* off, const int32_t*
 // workspace of batch * n ints.
 hipError_t solve_batched(int n, int nrhs, int64_t batch, double* M, double* R, int* piv,
                          hipStream_t st);
+// out_b = M_b^-1 (M untouched).  n <= 208: one workgroup per matrix (in-place Gauss-Jordan in
+// registers, partial pivoting); larger n: the blocked LU against the identity, on `work`
+// (batch n^2 doubles) with `piv` (batch n ints).
+hipError_t inverse_batched(int n, int64_t batch, const double* M, double* out, int* piv,
+                           double* work, hipStream_t st);
+constexpr int kInverseRegMax = 208;
 
 // out[b] = expm(A[b]) (expm.py:9-167).  Allocates its own workspace (stream-ordered).
 hipError_t expm_batched(int n, int64_t batch, const double* A, double* out, hipStream_t st);

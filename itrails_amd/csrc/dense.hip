@@ -740,6 +740,255 @@ hipError_t solve_batched(int n, int nrhs, int64_t batch, double* M, double* R, i
 }
 
 // ---------------------------------------------------------------------------------------
+// Inverse of an n x n matrix (n <= kGjMax) in one workgroup: in-place Gauss-Jordan
+// ---------------------------------------------------------------------------------------
+// The two inverses of a model build — Q^-1 of the deepest intervals (201 x 201 at (5,5)) and
+// the Pade denominator's diagonal block of the Van Loan evaluation (203 x 203) — ran as the
+// blocked LU above: ~50 dependent launches, ~0.55 ms each.  Here one workgroup holds the whole
+// matrix in registers (512 threads; thread (r, c) owns rows r + 32 mr and columns c + 16 mc)
+// and runs the n Gauss-Jordan steps with one barrier each: the pivot row and column go through
+// LDS, then every thread applies the rank-1 update to its 7 x 13 elements.
+//
+// Pivots follow partial pivoting (the first maximum |a_ik|, i >= k, like LAPACK's idamax).
+// Pass 1 takes the diagonal and checks at every step that no entry below it is larger in
+// magnitude — then partial pivoting would have chosen the same pivots, with no interchange
+// (the case for both matrices of the build).  If the check fails anywhere the workgroup
+// reloads the matrix and runs pass 2: a pivot search per step, row interchanges, and the
+// column interchanges of the in-place form in reverse order at the end.  The result is the
+// inverse of the matrix under that pivot sequence (rounding differs from getrf + getrs).
+constexpr int kGjR = 7, kGjC = 13;         // registers: rows r + 32 mr, columns c + 16 mc
+constexpr int kGjMax = 16 * kGjC;          // 208
+constexpr int kGjThreads = 512;
+
+struct GjShared {
+  double prow[2][kGjMax];  // the raw pivot row, by step parity
+  double pcol[2][32 * kGjR];  // the multipliers (pivot column; -1 at the pivot row)
+  double sw[2][32 * kGjR]; // row / column interchange buffers (pass 2; rows r + 32 mr <= 223)
+  double dk[2];            // the pivot, by step parity
+  double cval[32];
+  int cidx[32];
+  int piv[kGjMax];
+  int viol;
+};
+
+// a[m][*] / a[*][m] for a workgroup-uniform register index m (the pivoting pass only)
+template <int NR, int NC>
+__device__ __forceinline__ void gj_row_out(const double (&a)[NR][NC], int m, double* dst, int c) {
+#pragma unroll
+  for (int mm = 0; mm < NR; ++mm)
+    if (mm == m) {
+#pragma unroll
+      for (int mc = 0; mc < NC; ++mc) dst[c + 16 * mc] = a[mm][mc];
+    }
+}
+template <int NR, int NC>
+__device__ __forceinline__ void gj_row_in(double (&a)[NR][NC], int m, const double* src, int c) {
+#pragma unroll
+  for (int mm = 0; mm < NR; ++mm)
+    if (mm == m) {
+#pragma unroll
+      for (int mc = 0; mc < NC; ++mc) a[mm][mc] = src[c + 16 * mc];
+    }
+}
+template <int NR, int NC>
+__device__ __forceinline__ void gj_col_out(const double (&a)[NR][NC], int m, double* dst, int r) {
+#pragma unroll
+  for (int mc = 0; mc < NC; ++mc)
+    if (mc == m) {
+#pragma unroll
+      for (int mr = 0; mr < NR; ++mr) dst[r + 32 * mr] = a[mr][mc];
+    }
+}
+template <int NR, int NC>
+__device__ __forceinline__ void gj_col_in(double (&a)[NR][NC], int m, const double* src, int r) {
+#pragma unroll
+  for (int mc = 0; mc < NC; ++mc)
+    if (mc == m) {
+#pragma unroll
+      for (int mr = 0; mr < NR; ++mr) a[mr][mc] = src[r + 32 * mr];
+    }
+}
+
+// Step k of the elimination; MR = k >> 5 and MC = k >> 4 are compile-time register indices.
+// a_ij <- (j == k ? 0 : a_ij) - f_i P_j with f_i = a_ik (-1 at i = k) and P_j = a_kj / a_kk
+// (1 / a_kk at j = k): the pivot row becomes row / a_kk, the pivot column -a_ik / a_kk, the
+// pivot 1 / a_kk, every other entry a_ij - a_ik a_kj / a_kk.  (P_j = a_kj * (1 / a_kk): the
+// reciprocal multiplied, as LAPACK's getf2 scales its column.)
+template <int MR, int MC>
+__device__ __forceinline__ void gj_step(double (&a)[kGjR][kGjC], int k, int r, int c,
+                                        GjShared& sh, bool check) {
+  double* prow = sh.prow[k & 1];
+  double* pcol = sh.pcol[k & 1];
+  const bool own_row = r == (k & 31), own_col = c == (k & 15);
+  if (own_row) {  // the pivot itself goes to dk, its slot in prow holds 1 (P_k = 1 / a_kk)
+#pragma unroll
+    for (int mc = 0; mc < kGjC; ++mc) prow[c + 16 * mc] = c + 16 * mc == k ? 1.0 : a[MR][mc];
+    if (own_col) sh.dk[k & 1] = a[MR][MC];
+  }
+  if (own_col) {
+#pragma unroll
+    for (int mr = 0; mr < kGjR; ++mr) pcol[r + 32 * mr] = (r + 32 * mr == k) ? -1.0 : a[mr][MC];
+  }
+  __syncthreads();
+  const double d = sh.dk[k & 1];
+  const double inv = 1.0 / d;
+  if (own_col) {
+    if (check) {
+      bool bad = false;
+#pragma unroll
+      for (int mr = 0; mr < kGjR; ++mr) bad |= (r + 32 * mr > k) && fabs(a[mr][MC]) > fabs(d);
+      if (bad) sh.viol = 1;
+    }
+#pragma unroll
+    for (int mr = 0; mr < kGjR; ++mr) a[mr][MC] = 0.0;
+  }
+  if (own_row) {
+#pragma unroll
+    for (int mc = 0; mc < kGjC; ++mc) a[MR][mc] = 0.0;
+  }
+  double P[kGjC];
+#pragma unroll
+  for (int mc = 0; mc < kGjC; ++mc) P[mc] = prow[c + 16 * mc] * inv;
+#pragma unroll
+  for (int mr = 0; mr < kGjR; ++mr) {
+    const double f = pcol[r + 32 * mr];
+#pragma unroll
+    for (int mc = 0; mc < kGjC; ++mc) a[mr][mc] = fma(-f, P[mc], a[mr][mc]);
+  }
+}
+
+// pass 2's row interchange before step k (pivot search over column k, rows >= k)
+template <int MR, int MC>
+__device__ __forceinline__ void gj_pivot(double (&a)[kGjR][kGjC], int n, int k, int r, int c,
+                                         GjShared& sh) {
+  if (c == (k & 15)) {
+    double best = -1.0;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int mr = 0; mr < kGjR; ++mr) {  // rows ascend with mr: strict > keeps the first
+      const int i = r + 32 * mr;
+      const double v = fabs(a[mr][MC]);
+      if (i >= k && i < n && v > best) {
+        best = v;
+        bi = i;
+      }
+    }
+    sh.cval[r] = best;
+    sh.cidx[r] = bi;
+  }
+  __syncthreads();
+  double best = -1.0;
+  int p = k;
+  for (int u = 0; u < 32; ++u) {
+    const double v = sh.cval[u];
+    const int i = sh.cidx[u];
+    if (v > best || (v == best && i < p)) {
+      best = v;
+      p = i;
+    }
+  }
+  p = __builtin_amdgcn_readfirstlane(p);
+  if (threadIdx.x == 0) sh.piv[k] = p;
+  if (p != k) {
+    if (r == (k & 31)) gj_row_out(a, MR, sh.sw[0], c);
+    if (r == (p & 31)) gj_row_out(a, p >> 5, sh.sw[1], c);
+    __syncthreads();
+    if (r == (k & 31)) gj_row_in(a, MR, sh.sw[1], c);
+    if (r == (p & 31)) gj_row_in(a, p >> 5, sh.sw[0], c);
+  }
+  __syncthreads();  // (cval / sw are rewritten by the next step)
+}
+
+// steps 16 MC .. 16 MC + 15 (register indices MR = MC / 2, MC), then the next 16
+template <int MC, bool PIVOT>
+__device__ __forceinline__ void gj_sweep(double (&a)[kGjR][kGjC], int n, int r, int c,
+                                         GjShared& sh) {
+  if constexpr (MC < kGjC) {
+    for (int k = 16 * MC; k < 16 * MC + 16 && k < n; ++k) {
+      if (PIVOT) gj_pivot<MC / 2, MC>(a, n, k, r, c, sh);
+      gj_step<MC / 2, MC>(a, k, r, c, sh, !PIVOT);
+    }
+    gj_sweep<MC + 1, PIVOT>(a, n, r, c, sh);
+  }
+}
+
+// PIVOT = false: pass 1, flag[b] = 1 where partial pivoting would interchange rows;
+// PIVOT = true: pass 2 for the flagged matrices only (a launch of its own, so that its
+// run-time register indices — the interchanged rows and columns — do not push pass 1's
+// matrix out of registers; the flagged case does not occur in the model build)
+template <bool PIVOT>
+__global__ void __launch_bounds__(kGjThreads) gj_inverse_kernel(int n, const double* Mb,
+                                                                double* Ob, int* flag) {
+  __shared__ GjShared sh;
+  if (PIVOT && flag[blockIdx.x] == 0) return;
+  const double* M = Mb + (int64_t)blockIdx.x * n * n;
+  double* O = Ob + (int64_t)blockIdx.x * n * n;
+  const int r = threadIdx.x & 31, c = threadIdx.x >> 5;
+  double a[kGjR][kGjC];
+#pragma unroll
+  for (int mr = 0; mr < kGjR; ++mr)
+#pragma unroll
+    for (int mc = 0; mc < kGjC; ++mc) {
+      const int i = r + 32 * mr, j = c + 16 * mc;
+      a[mr][mc] = (i < n && j < n) ? M[(int64_t)i * n + j] : 0.0;
+    }
+  if (threadIdx.x == 0) sh.viol = 0;
+  __syncthreads();
+  gj_sweep<0, PIVOT>(a, n, r, c, sh);
+  __syncthreads();
+  if (!PIVOT) {
+    if (threadIdx.x == 0) flag[blockIdx.x] = sh.viol;
+  } else {
+    for (int k = n - 1; k >= 0; --k) {  // X P: column interchanges in reverse order
+      const int p = sh.piv[k];
+      if (p == k) continue;
+      if (c == (k & 15)) gj_col_out(a, k >> 4, sh.sw[0], r);
+      if (c == (p & 15)) gj_col_out(a, p >> 4, sh.sw[1], r);
+      __syncthreads();
+      if (c == (k & 15)) gj_col_in(a, k >> 4, sh.sw[1], r);
+      if (c == (p & 15)) gj_col_in(a, p >> 4, sh.sw[0], r);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int mr = 0; mr < kGjR; ++mr)
+#pragma unroll
+    for (int mc = 0; mc < kGjC; ++mc) {
+      const int i = r + 32 * mr, j = c + 16 * mc;
+      if (i < n && j < n) O[(int64_t)i * n + j] = a[mr][mc];
+    }
+}
+
+__global__ void __launch_bounds__(256) identity_kernel(int n, int64_t batch, double* R) {
+  const int64_t nn = (int64_t)n * n;
+  for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < batch * nn; e += (int64_t)gridDim.x * 256) {
+    const int64_t q = e % nn;
+    R[e] = (q / n == q % n) ? 1.0 : 0.0;
+  }
+}
+
+hipError_t inverse_batched(int n, int64_t batch, const double* M, double* out, int* piv,
+                           double* work, hipStream_t st) {
+  if (batch <= 0 || n <= 0) return hipSuccess;
+  if (n <= kGjMax) {  // piv: one flag per matrix
+    for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+      const int nb = (int)std::min<int64_t>(65535, batch - b0);
+      hipLaunchKernelGGL(gj_inverse_kernel<false>, dim3(nb), dim3(kGjThreads), 0, st, n,
+                         M + b0 * n * n, out + b0 * n * n, piv + b0);
+      hipLaunchKernelGGL(gj_inverse_kernel<true>, dim3(nb), dim3(kGjThreads), 0, st, n,
+                         M + b0 * n * n, out + b0 * n * n, piv + b0);
+    }
+    return hipGetLastError();
+  }
+  // larger orders: the blocked LU on a copy, against the identity
+  if (hipError_t e = hipMemcpyAsync(work, M, (size_t)batch * n * n * sizeof(double),
+                                    hipMemcpyDeviceToDevice, st))
+    return e;
+  hipLaunchKernelGGL(identity_kernel, dim3(1024), dim3(256), 0, st, n, batch, out);
+  return solve_batched(n, n, batch, work, out, piv, st);
+}
+
+// ---------------------------------------------------------------------------------------
 // expm
 // ---------------------------------------------------------------------------------------
 // Pade coefficients b_0 .. b_m (Higham 2008, Alg. 10.20; the values of expm.py:29-140)

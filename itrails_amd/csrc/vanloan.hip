@@ -1099,6 +1099,11 @@ hipError_t vanloan_paths(int nb, const double* h_Q, int njobs, const double* h_t
       hipLaunchKernelGGL(member_lincomb_kernel, dim3(grid), dim3(256), 0, st, a);
     } else if (ln.kind == 2) {
       const int g0 = P.H[ln.a0], nr = P.H[ln.a0 + 1];
+      if (nb <= kInverseRegMax) {  // one workgroup per root in registers (dense.hip)
+        if ((e = inverse_batched(nb, nr, Wb[1] + P.moff[g0], Wb[NINV], piv, nullptr, st)))
+          return e;
+        continue;
+      }
       LinArgs a{};
       a.nb = nb;
       a.count = nr * nn;

@@ -19,7 +19,7 @@ import numpy as np
 from ._lib import check, lib
 
 __all__ = ["expm", "expm_batched", "expm_blocktri_batched", "vanloan_paths", "vanloan_job_norms",
-           "solve_batched", "gemm_batched"]
+           "solve_batched", "inverse_batched", "gemm_batched"]
 
 
 def _dev(x):
@@ -146,6 +146,20 @@ def solve_batched(M, R):
         check(lib().itr_solve_batched(dM.shape[1], dR.shape[2], dM.shape[0], dM.data_ptr(),
                                       dR.data_ptr(), _stream()))
     return dR if on_dev else dR.cpu().numpy()
+
+
+def inverse_batched(M):
+    """M[b]^-1 for every b (itr_inverse_batched: Gauss-Jordan in registers for n <= 208)."""
+    import torch
+    dM, on_dev = _dev(M)
+    if dM.dim() != 3 or dM.shape[1] != dM.shape[2]:
+        raise ValueError("expected M (batch, n, n)")
+    dM = dM.contiguous()
+    out = torch.empty_like(dM)
+    if dM.shape[0]:
+        check(lib().itr_inverse_batched(dM.shape[1], dM.shape[0], dM.data_ptr(), out.data_ptr(),
+                                        _stream()))
+    return out if on_dev else out.cpu().numpy()
 
 
 def gemm_batched(A, B, alpha=1.0):

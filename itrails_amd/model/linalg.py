@@ -118,10 +118,10 @@ class DeviceLinalg:
         215-256): (-C^-1)[:n, -n:] @ A_{L-1} for the block upper bidiagonal C of path p
         (diagonal blocks Q, super-diagonal A_i = diag(m p[i-1]) Q diag(m p[i])).  The top-right
         block of the inverse of such a matrix is (-1)^(L-2) Q^-1 A_1 Q^-1 ... A_{L-2} Q^-1, so
-        the integral is (-1)^(L-1) G_1 G_2 ... G_{L-1} with G_i = Q^-1 A_i: one LU inverse of
+        the integral is (-1)^(L-1) G_1 G_2 ... G_{L-1} with G_i = Q^-1 A_i: one inverse of
         Q, one batched GEMM for every distinct omega pair, then the chain products per path
         length (MFMA GEMMs, dense.hip) — instead of one LU of order (L-1) n per path."""
-        from ..dense import gemm_batched, solve_batched
+        from ..dense import gemm_batched, inverse_batched
         torch = self.torch
         n = Q.shape[0]
         out = torch.empty((len(paths), n, n), dtype=torch.float64, device=self.dev)
@@ -129,7 +129,7 @@ class DeviceLinalg:
             return out
         plan = self._deepest_plan(masks, paths, n)
         dQ = torch.from_numpy(np.ascontiguousarray(Q)).to(self.dev)
-        Qinv = solve_batched(dQ[None].clone(), plan["eye"][None].clone())[0]
+        Qinv = inverse_batched(dQ[None])[0]
         A = (plan["ma"][:, :, None] * dQ[None] * plan["mb"][:, None, :]).contiguous()
         G = gemm_batched(Qinv.expand(A.shape[0], n, n).contiguous(), A)
         for L, idx, cols in plan["by_len"]:
@@ -167,8 +167,7 @@ class DeviceLinalg:
             steps.append((L, torch.as_tensor(idx, device=dev),
                           [torch.from_numpy(np.ascontiguousarray(gi[:, k])).to(dev)
                            for k in range(L - 1)]))
-        plan = {"ma": ma, "mb": mb, "by_len": steps,
-                "eye": torch.eye(n, dtype=torch.float64, device=dev)}
+        plan = {"ma": ma, "mb": mb, "by_len": steps}
         if len(cache) > 8:
             cache.clear()
         cache[key] = plan

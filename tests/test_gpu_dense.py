@@ -60,6 +60,45 @@ def test_solve_needs_pivoting(gpu):
     assert np.allclose(solve_batched(M, R)[0], np.linalg.inv(M[0]), rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("n,batch,dominant", [(1, 3, True), (2, 2, False), (7, 3, False),
+                                              (31, 2, True), (33, 3, False), (64, 2, False),
+                                              (201, 2, True), (203, 3, False), (208, 2, True),
+                                              (208, 1, False), (230, 2, False)])
+def test_inverse_matches_lapack(gpu, n, batch, dominant):
+    """itr_inverse_batched against LAPACK's inverse: diagonally dominant matrices take the
+    pass without interchanges, general ones (and one dominant member beside them) the
+    pivoting pass; n = 230 the blocked-LU fallback."""
+    from itrails_amd.dense import inverse_batched
+    rng = np.random.default_rng(n * 7 + batch)
+    M = rng.standard_normal((batch, n, n))
+    if dominant:
+        M += np.eye(n) * (np.abs(M).sum(axis=1, keepdims=True) + 1.0)
+    elif batch > 1:
+        M[0] += np.eye(n) * (np.abs(M[0]).sum(axis=0) + 1.0)  # a pass-1 member in the batch
+    X = inverse_batched(M)
+    ref = np.linalg.inv(M)
+    for b in range(batch):
+        err = np.abs(X[b] - ref[b]).max() / np.abs(ref[b]).max()
+        assert err < 1e-11 * max(1.0, np.linalg.cond(M[b]) / 1e3), (n, b, err)
+
+
+def test_inverse_pivoting_pattern(gpu):
+    """A zero leading pivot and interchanges at several steps (the pivoting pass's row and
+    column interchanges), and the model build's matrix shape: a rate matrix of order 201."""
+    from itrails_amd.dense import inverse_batched
+    M = np.array([[[0.0, 1.0, 2.0], [3.0, 4.0, 5.0], [6.0, 7.0, 9.0]]])
+    assert np.allclose(inverse_batched(M)[0], np.linalg.inv(M[0]), rtol=1e-12, atol=1e-12)
+    rng = np.random.default_rng(5)
+    P = np.eye(64)[rng.permutation(64)]
+    A = P @ (np.eye(64) * 10 + rng.standard_normal((64, 64)))  # rows shuffled: swaps needed
+    assert np.allclose(inverse_batched(A[None])[0], np.linalg.inv(A), rtol=1e-10, atol=1e-12)
+    Q = rng.random((201, 201)) * (rng.random((201, 201)) < 0.05)
+    np.fill_diagonal(Q, 0.0)
+    np.fill_diagonal(Q, -Q.sum(axis=1) - rng.random(201) * 0.1)
+    ref = np.linalg.inv(Q)
+    assert np.allclose(inverse_batched(Q[None])[0], ref, rtol=1e-11, atol=1e-13 * np.abs(ref).max())
+
+
 @pytest.mark.parametrize("m,n,k", [(1, 1, 1), (1, 203, 203), (203, 203, 203), (70, 17, 129),
                                    (64, 64, 16), (65, 63, 17)])
 def test_gemm_matches_blas(gpu, m, n, k):
