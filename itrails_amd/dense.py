@@ -22,13 +22,44 @@ __all__ = ["expm", "expm_batched", "expm_blocktri_batched", "vanloan_paths", "va
            "solve_batched", "inverse_batched", "gemm_batched"]
 
 
+_PINNED: dict = {}  # shape -> ring of [pinned host tensor, event of its last copy]
+_RING = 4
+
+
+def h2d(x):
+    """A float64 host array on the current device without a host-side wait: the copy goes
+    through a pinned staging buffer (a ring of four per shape, each reused only after its
+    previous copy is done).  A copy from pageable memory would wait for every kernel queued
+    before it on the stream, so each one in the model build stalled the host until the
+    device was idle."""
+    import torch
+    a = np.ascontiguousarray(x, dtype=np.float64)
+    ring = _PINNED.get(a.shape)
+    if ring is None:
+        if len(_PINNED) > 64:
+            _PINNED.clear()
+        ring = _PINNED[a.shape] = [0, [[torch.empty(a.shape, dtype=torch.float64,
+                                                    pin_memory=True), None]
+                                       for _ in range(_RING)]]
+    slot = ring[1][ring[0]]
+    ring[0] = (ring[0] + 1) % _RING
+    if slot[1] is not None:
+        slot[1].synchronize()
+    slot[0].numpy()[...] = a
+    out = slot[0].to("cuda", non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    slot[1] = ev
+    return out
+
+
 def _dev(x):
     import torch
     if isinstance(x, torch.Tensor):
         if not x.is_cuda or x.dtype != torch.float64:
             raise TypeError("expected a torch.cuda float64 tensor")
         return x.contiguous(), True
-    return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64)).cuda(), False
+    return h2d(x), False
 
 
 def _stream():

@@ -795,6 +795,7 @@ def _run_chain_abc_device(plan, Q, times, ss, probs: Dict, la) -> Dict:
     [rows, n] tensor advanced interval by interval, the closing phase's contractions; a
     single device-to-host copy of the final per-key probabilities."""
     import torch
+    from ..dense import h2d
     tab = _device_tables(plan, Q, ss, la)
     masks = ss.omega_masks
     n = Q.shape[0]
@@ -815,7 +816,7 @@ def _run_chain_abc_device(plan, Q, times, ss, probs: Dict, la) -> Dict:
     P0 = np.zeros((len(probs), n))
     for i, v in enumerate(probs.values()):
         P0[i] = v[0]
-    P[:len(probs)] = torch.from_numpy(P0).to(dev)
+    P[:len(probs)] = h2d(P0) if P.is_cuda else torch.from_numpy(P0)
     for d, (E, M) in zip(tab["ivs"], EM):
         # (P * mask) @ propagator * mask for every key row of the interval, gathered, multiplied
         # and scattered by one fused kernel per matrix kind (itr_chain_rows)

@@ -97,11 +97,18 @@ def single_table(t: float, mu: float, k: float) -> np.ndarray:
     (p_b_c_given_a_JC69_analytical, get_emission_prob_mat.py:73-90).
     (1/4 + al x)(1/4 + be x)(1/4 + ga e^{-mu t} / x), x = e^{-mu s}, weight e^{-ks}: six
     exponential terms whose coefficient arrays are fixed, so one weighted sum of them."""
+    return single_tables([(t, mu, k)])[0]
+
+
+def single_tables(keys) -> np.ndarray:
+    """single_table of every (t, mu, k) in `keys` at once: (K, 4, 4, 4)."""
     C, flag, mpow = _single_coeffs()
+    kt = np.asarray(keys, dtype=np.float64).reshape(-1, 3)
+    t, mu, k = kt[:, 0:1], kt[:, 1:2], kt[:, 2:3]
     emt = np.exp(-mu * t)
     w = np.where(flag == 1, emt, 1.0) * _phi(-k + mu * mpow, t)
     val = k * (w @ C) / (1 - np.exp(-(k * t)))
-    return val.reshape(4, 4, 4, 4).sum(axis=3)
+    return val.reshape(-1, 4, 4, 4, 4).sum(axis=4)
 
 
 def _double_coeffs():
@@ -140,7 +147,14 @@ def double_table(t: float, mu: float) -> np.ndarray:
     Factors in s1, s2: e^{-2 s1} e^{-s2}, (1/4 + al y1)(1/4 + be y1), (1/4 + ga y2 / y1),
     (1/4 + de y2), (1/4 + ep e^{-mu t} / y2) with y1 = e^{-mu s1}, y2 = e^{-mu s2}: 24
     exponential terms with fixed coefficient arrays, one weighted sum of them."""
+    return double_tables([(t, mu)])[0]
+
+
+def double_tables(keys) -> np.ndarray:
+    """double_table of every (t, mu) in `keys` at once: (K, 4, 4, 4, 4)."""
     C, pq, quv, flag = _double_coeffs()
+    tm = np.asarray(keys, dtype=np.float64).reshape(-1, 2)
+    t, mu = tm[:, 0:1], tm[:, 1:2]
     emt = np.exp(-mu * t)
     lam1 = -2.0 - mu * pq
     lam2 = -1.0 - mu * quv
@@ -154,7 +168,7 @@ def double_table(t: float, mu: float) -> np.ndarray:
                                   t * t / 2))
     w = np.where(flag, emt, 1.0) * inner
     den = 1 + 0.5 / np.exp(3 * t) - 1.5 / np.exp(t)
-    val = (3 * (w @ C) / den).reshape(4, 4, 4, 4, 16)
+    val = (3 * (w @ C) / den).reshape(-1, 4, 4, 4, 4, 16)
     # the 16 (e, f) terms summed one after another, e outer, like the reference's cumsum
     # (get_emission_prob_mat.py:417-423); NumPy's sum over 16 would pair them
     out = val[..., 0].copy()
@@ -273,20 +287,25 @@ def emission_rows(specs, la=None) -> Tuple[List[tuple], np.ndarray]:
                 gens.append(m)
     P = la.expm(list(generator_matrices(gens)))
     tab = np.zeros((len(specs), ET_STRIDE))
-    slot = [ET_A, ET_B, ET_C, ET_D, ET_AB]
-    for (s, g), m in zip(where, P):
-        tab[s, slot[g]:slot[g] + 16] = m.reshape(-1)
+    slot = np.array([ET_A, ET_B, ET_C, ET_D, ET_AB])
+    if where:
+        wi = np.asarray(where, dtype=np.int64)
+        cols = slot[wi[:, 1]][:, None] + np.arange(16)
+        tab[wi[:, 0:1], cols] = np.stack(P).reshape(len(P), 16)
+    # the distinct coalescence tables of the build, each kind in one vectorised evaluation
+    skeys = list(dict.fromkeys(k for sp in specs if sp[1] == 0 for k in (sp[4], sp[5])))
+    dkeys = list(dict.fromkeys(sp[6] for sp in specs if sp[1] != 0))
     cache = {}
+    if skeys:
+        cache.update(zip(skeys, single_tables(skeys).reshape(len(skeys), 64)))
+    if dkeys:
+        cache.update(zip(dkeys, double_tables(dkeys).reshape(len(dkeys), 256)))
     for s, (state, kind, perm, _, first, second, dbl) in enumerate(specs):
         tab[s, ET_KIND] = kind
         tab[s, ET_PERM] = perm
         if kind == 0:
-            for key, off in ((first, ET_F), (second, ET_S)):
-                if key not in cache:
-                    cache[key] = single_table(*key).reshape(-1)
-                tab[s, off:off + 64] = cache[key]
+            tab[s, ET_F:ET_F + 64] = cache[first]
+            tab[s, ET_S:ET_S + 64] = cache[second]
         else:
-            if dbl not in cache:
-                cache[dbl] = double_table(*dbl).reshape(-1)
             tab[s, ET_DD:ET_DD + 256] = cache[dbl]
     return [sp[0] for sp in specs], la.emission_rows(tab)

@@ -121,14 +121,14 @@ class DeviceLinalg:
         the integral is (-1)^(L-1) G_1 G_2 ... G_{L-1} with G_i = Q^-1 A_i: one inverse of
         Q, one batched GEMM for every distinct omega pair, then the chain products per path
         length (MFMA GEMMs, dense.hip) — instead of one LU of order (L-1) n per path."""
-        from ..dense import gemm_batched, inverse_batched
+        from ..dense import gemm_batched, h2d, inverse_batched
         torch = self.torch
         n = Q.shape[0]
         out = torch.empty((len(paths), n, n), dtype=torch.float64, device=self.dev)
         if not len(paths):
             return out
         plan = self._deepest_plan(masks, paths, n)
-        dQ = torch.from_numpy(np.ascontiguousarray(Q)).to(self.dev)
+        dQ = h2d(Q)
         Qinv = inverse_batched(dQ[None])[0]
         A = (plan["ma"][:, :, None] * dQ[None] * plan["mb"][:, None, :]).contiguous()
         G = gemm_batched(Qinv.expand(A.shape[0], n, n).contiguous(), A)
@@ -215,7 +215,8 @@ class DeviceLinalg:
         """Emission rows of every state from its packed tables (emission.hip)."""
         from .._lib import check, lib
         torch = self.torch
-        dt = torch.from_numpy(np.ascontiguousarray(tables, dtype=np.float64)).to(self.dev)
+        from ..dense import h2d
+        dt = h2d(tables)
         out = torch.empty((tables.shape[0], 256), dtype=torch.float64, device=self.dev)
         check(lib().itr_emission_rows(tables.shape[0], dt.data_ptr(), out.data_ptr(),
                                       torch.cuda.current_stream().cuda_stream))

@@ -2,7 +2,7 @@
 # timeline.
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r6m
+O=gpurun_out/${TAG:-r6m}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_dense.py tests/test_gpu_model.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
@@ -17,3 +17,4 @@ python scripts/build_timeline.py analyse $f > $O/analysis.txt 2>&1
 cp $f $O/kernel_trace.csv
 rm -rf $O/bt
 head -25 $O/analysis.txt
+timeout -k 10 200 python scripts/build_stages.py 5 30 > $O/stages.txt 2>&1 && cat $O/stages.txt
