@@ -1,5 +1,5 @@
-"""Lone-block Viterbi step latency: one block of T columns ((5,5) KAT model), the Viterbi
-sweep's kernel time / T.  usage: python scripts/vit_lone.py [T] [nblocks]"""
+"""Lone-block Viterbi step latency: one block of T columns ((n,n) KAT model, default (5,5)),
+the Viterbi sweep's kernel time / T.  usage: python scripts/vit_lone.py [T] [nblocks] [n_int]"""
 import os
 import sys
 
@@ -16,7 +16,8 @@ from itrails_amd.synth import sample_alignment  # noqa: E402
 def main():
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 18377
     nb = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    a, b, pi, _ = bench.load_model(5)
+    n_int = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    a, b, pi, _ = bench.load_model(n_int)
     obs, off, _ = sample_alignment(a, b, pi, [T] * nb, seed=5)
     model = hmm.Model(a, b, pi)
     plan = hmm.Plan(off)
@@ -30,7 +31,7 @@ def main():
         hmm.viterbi_device(model, plan, d_obs, out=d_path)
         ms.append(hmm.last_kernel_ms("viterbi"))
     m = min(ms)
-    print(f"cfg {os.environ.get('ITR_VIT_CFG', 'default')} T {T} blocks {nb}: viterbi {m:.3f} ms"
+    print(f"N {a.shape[0]} cfg {os.environ.get('ITR_VIT_CFG', 'default')} T {T} blocks {nb}: viterbi {m:.3f} ms"
           f" = {m * 1e6 / T:.1f} ns/step")
 
 
