@@ -1,5 +1,5 @@
 """Lone-block Viterbi step latency: one block of T columns ((n,n) KAT model, default (5,5)),
-the Viterbi sweep's kernel time / T.  usage: python scripts/vit_lone.py [T] [nblocks] [n_int]"""
+the Viterbi sweep's kernel time / T.  usage: python scripts/vit_lone.py [T] [nblocks] [n_int | i<n_int> (introgression)]"""
 import os
 import sys
 
@@ -16,8 +16,11 @@ from itrails_amd.synth import sample_alignment  # noqa: E402
 def main():
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 18377
     nb = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    n_int = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-    a, b, pi, _ = bench.load_model(n_int)
+    arg = sys.argv[3] if len(sys.argv) > 3 else "5"
+    if arg.startswith("i"):  # the introgression model, e.g. i5 (N = 95)
+        a, b, pi, _ = bench.load_model_intro(int(arg[1:]))
+    else:
+        a, b, pi, _ = bench.load_model(int(arg))
     obs, off, _ = sample_alignment(a, b, pi, [T] * nb, seed=5)
     model = hmm.Model(a, b, pi)
     plan = hmm.Plan(off)
