@@ -66,7 +66,11 @@ class StateSpace:
 
     def rate_matrix(self, coal: float, rho: float) -> np.ndarray:
         """Q[from, to] = coal or rho; Q[i, i] = -sum of row i (trans_mat.py:487-508), the row
-        sum accumulated left to right like the reference's loop (np.cumsum is sequential)."""
+        sum accumulated left to right like the reference's loop (np.cumsum is sequential).
+        The last result is kept (read-only): a build asks for the same matrix twice."""
+        last = self.__dict__.get("_rm_last")
+        if last is not None and last[0] == (coal, rho):
+            return last[1]
         n = self.n
         idx = self.__dict__.get("_tr_idx")
         if idx is None:
@@ -78,6 +82,8 @@ class StateSpace:
         Q[f, t] = np.where(is_rho, rho, coal)
         d = np.arange(n)
         Q[d, d] = -np.cumsum(Q, axis=1)[:, -1]
+        Q.flags.writeable = False
+        object.__setattr__(self, "_rm_last", ((coal, rho), Q))
         return Q
 
 
