@@ -933,6 +933,20 @@ def _close_deepest(Q, ss, probs: Dict, n_int, la) -> Dict:
     return out
 
 
+def _expm2(Q, t):
+    """expm(Q t) of a two-state rate matrix [[-a, a], [b, -b]] in closed form:
+    (1/s) [[b + a e, a (1 - e)], [b (1 - e), a + b e]] with s = a + b, e = e^{-s t} (within a
+    few ulp of expm.py's Pade evaluation, get_joint_prob_mat.py:119-123; no device round trip
+    for three 2 x 2 matrices)."""
+    a, b = Q[0, 1], Q[1, 0]
+    sr = a + b
+    if sr == 0.0:
+        return np.eye(2)
+    om = -np.expm1(-sr * t)  # 1 - e
+    e = 1.0 - om
+    return np.array([[b + a * e, a * om], [b * om, a + b * e]]) / sr
+
+
 def joint_prob_mat(t_A, t_B, t_AB, t_C, rho_A, rho_B, rho_AB, rho_C, rho_ABC, coal_A, coal_B,
                    coal_AB, coal_C, coal_ABC, n_int_AB, n_int_ABC, cut_AB, cut_ABC,
                    la=None) -> Dict:
@@ -948,7 +962,7 @@ def joint_prob_mat(t_A, t_B, t_AB, t_C, rho_A, rho_B, rho_AB, rho_C, rho_ABC, co
     Qabc = s3.rate_matrix(coal_ABC, rho_ABC)
     pi1 = np.zeros(2)
     pi1[s1.index[(1, 1)]] = 1.0
-    Ea, Eb, Ec = la.expm([Qa * t_A, Qb * t_B, Qc * t_C])
+    Ea, Eb, Ec = (_expm2(Qa, t_A), _expm2(Qb, t_B), _expm2(Qc, t_C))
     fa = (pi1 @ Ea).reshape(1, -1)
     fb = (pi1 @ Eb).reshape(1, -1)
     fc = (pi1 @ Ec).reshape(1, -1)
