@@ -102,3 +102,23 @@ def test_coalescence_tables_vs_reference_closed_forms():
         if mu > 0.1:
             np.testing.assert_allclose(s, S, rtol=1e-12, atol=0)
             np.testing.assert_allclose(d, D, rtol=1e-12, atol=0)
+
+
+def test_closed_form_propagators_vs_expm():
+    """The host's closed forms of the build's small exponentials against scipy's expm: the
+    JC69-form branch generators (emissions.jc69_propagators) and the one-species two-state
+    chains (chains._expm2), within a few ulp of the matrix scale."""
+    import scipy.linalg as sl
+    from itrails_amd.model.chains import _expm2
+    from itrails_amd.model.emissions import generator_matrices, jc69_propagators
+    from itrails_amd.model.statespace import state_space
+    rng = np.random.default_rng(3)
+    gens = [(a, -3.0 * a) for a in rng.random(50) * 2.0] + [(0.0, 0.0), (0.3, -0.7)]
+    P = jc69_propagators(gens)
+    for g, m in zip(gens, generator_matrices(gens)):
+        ref = sl.expm(m)
+        assert np.abs(P[gens.index(g)] - ref).max() <= 5e-14 * np.abs(ref).max()
+    for coal, rho, t in [(0.7, 0.3, 0.5), (1.2, 1e-3, 3.0), (1.0, 2.0, 1e-4), (0.0, 0.0, 1.0)]:
+        Q = state_space(1).rate_matrix(coal, rho)
+        ref = sl.expm(Q * t)
+        assert np.abs(_expm2(Q, t) - ref).max() <= 5e-14 * np.abs(ref).max()
