@@ -115,6 +115,15 @@ struct Partitions {
 };
 thread_local Partitions g_parts;
 
+// the calling thread's partition of the current device (nullptr: none yet)
+Partition* current_partition() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  for (auto& x : g_parts.v)
+    if (x.device == dev) return &x;
+  return nullptr;
+}
+
 // lng on `reserve` CUs, lng2 on `reserve2` others (0: lng2 on lng's CUs), blk on the rest
 int partition(int reserve, int reserve2, Partition** out, bool masked = true) {
   int dev = 0;
@@ -613,54 +622,46 @@ int forward_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* logli
       // the chip (masked streams: a group workgroup beside a running half slows it down)
       const int ncu = cu_count();
       const int X = (ncu % 8 == 0) ? 8 : 1;
-      const int rfr = (int)std::min<int64_t>((p->nutasks + X - 1) / X * X, ncu / 4);
+      int rfr = (int)std::min<int64_t>((p->nutasks + X - 1) / X * X, ncu / 4);
       Partition* pt = nullptr;
-      if (int e = partition(0, rfr, &pt)) return e;
+      int rv = 0;  // a Viterbi set left by a forward + Viterbi call: matrix-core groups there too
+      // The thread keeps one partition per device; re-creating its CU-masked streams for each
+      // call of an alternating loglik / viterbi sequence (the host-block wrappers) cost ~40 ms
+      // a call, so the forward takes the forward + Viterbi call's partition when there is one.
+      // (a partition without a second set has lng2 on lng's CUs: the halves go there)
+      if (Partition* cur = current_partition())
+        if (cur->masked && cur->reserve > 0) {
+          pt = cur;
+          rv = cur->reserve2 > 0 ? cur->reserve : 0;
+          rfr = cur->reserve2 > 0 ? cur->reserve2 : cur->reserve;
+        }
+      if (!pt)
+        if (int e = partition(0, rfr, &pt)) return e;
       Scope sc("forward", st);
       HIP_TRY(hipMemsetAsync(p->d_queue + 3, 0, 2 * sizeof(int), st));
       HIP_TRY(hipEventRecord(pt->fork, st));
       HIP_TRY(hipStreamWaitEvent(pt->lng2, pt->fork, 0));
       HIP_TRY(hipStreamWaitEvent(pt->blk, pt->fork, 0));
-#ifdef ITR_EXPERIMENT
-      // the groups on the per-wave forward (wave_tasks.h fwd_wave_task) instead of the hybrid
-      const itr::WaveMfmaGeometry wf = itr::wave_mfma_geometry(m->n);
-      if (getenv("ITR_WAVE_FWD") && wf.cfg >= 0 && m->EF) {
-        itr::WaveMfmaArgs f{};
-        f.n = m->n;
-        f.ngroups = p->ngroups_ll;
-        f.groups = p->d_groups_ll;
-        f.tasks = p->d_mtasks;
-        f.queue = p->d_queue + 4;
-        f.off = p->d_off;
-        f.obs = obs;
-        f.a = m->a;
-        f.aT = m->aT;
-        f.ef = m->EF;
-        f.emit = m->E;
-        f.init = m->PIE;
-        f.loglik = loglik;
-        f.svec = p->d_svec;
-        f.sstride = g.xr;
-        f.sK = p->d_sK;
-        f.prio_len = INT32_MAX;
-        HIP_TRY(itr::launch_wave_mfma(wf, wf.per_cu * (ncu - rfr), f, pt->blk));
-        if (int e = run_valu_forward(m, p, a, g, pt->lng2, rfr, false)) return e;
-        HIP_TRY(itr::launch_wave_mfma(wf, wf.per_cu * rfr, f, pt->lng2));
-      } else
-#endif
-      {
-        if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->blk, nullptr, false, true,
-                               (int64_t)g.per_cu * (ncu - rfr), false, ncu - rfr))
+      if (rv > 0) HIP_TRY(hipStreamWaitEvent(pt->lng, pt->fork, 0));
+      if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->blk, nullptr, false, true,
+                             (int64_t)g.per_cu * (ncu - rfr - rv), false, ncu - rfr - rv))
+        return e;
+      if (rv > 0)
+        if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->lng, nullptr, false, true,
+                               (int64_t)g.per_cu * rv, false, rv))
           return e;
-        if (int e = run_valu_forward(m, p, a, g, pt->lng2, rfr, false)) return e;
-        if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->lng2, nullptr, false, true,
-                               (int64_t)g.per_cu * rfr, false, rfr))
-          return e;
-      }
+      if (int e = run_valu_forward(m, p, a, g, pt->lng2, rfr, false)) return e;
+      if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->lng2, nullptr, false, true,
+                             (int64_t)g.per_cu * rfr, false, rfr))
+        return e;
       HIP_TRY(hipEventRecord(pt->jl2, pt->lng2));
       HIP_TRY(hipEventRecord(pt->jb, pt->blk));
       HIP_TRY(hipStreamWaitEvent(st, pt->jl2, 0));
       HIP_TRY(hipStreamWaitEvent(st, pt->jb, 0));
+      if (rv > 0) {
+        HIP_TRY(hipEventRecord(pt->jl, pt->lng));
+        HIP_TRY(hipStreamWaitEvent(st, pt->jl, 0));
+      }
     } else if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, st, "forward", true, true, -1,
                                   true, cus)) {
       return e;
