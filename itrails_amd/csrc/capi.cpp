@@ -625,6 +625,7 @@ int forward_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* logli
       int rfr = (int)std::min<int64_t>((p->nutasks + X - 1) / X * X, ncu / 4);
       Partition* pt = nullptr;
       int rv = 0;  // a Viterbi set left by a forward + Viterbi call: matrix-core groups there too
+      bool reused = false;
       // The thread keeps one partition per device; re-creating its CU-masked streams for each
       // call of an alternating loglik / viterbi sequence (the host-block wrappers) cost ~40 ms
       // a call, so the forward takes the forward + Viterbi call's partition when there is one.
@@ -632,6 +633,7 @@ int forward_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* logli
       if (Partition* cur = current_partition())
         if (cur->masked && cur->reserve > 0) {
           pt = cur;
+          reused = true;
           rv = cur->reserve2 > 0 ? cur->reserve : 0;
           rfr = cur->reserve2 > 0 ? cur->reserve2 : cur->reserve;
         }
@@ -650,7 +652,11 @@ int forward_impl(itr_model_t m, itr_plan_t p, const uint16_t* obs, double* logli
         if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->lng, nullptr, false, true,
                                (int64_t)g.per_cu * rv, false, rv))
           return e;
-      if (int e = run_valu_forward(m, p, a, g, pt->lng2, rfr, false)) return e;
+      // (on a forward + Viterbi partition the set was sized for fwd_per_cu halves per CU)
+      const int64_t fg = reused ? std::max<int64_t>(rfr, std::min<int64_t>(
+                                      p->nutasks, (int64_t)std::max(1, p->fwd_per_cu) * rfr))
+                                : rfr;
+      if (int e = run_valu_forward(m, p, a, g, pt->lng2, fg, fg > rfr)) return e;
       if (int e = run_hybrid(itr::MODE_FWD_LL, m, p, a, g, pt->lng2, nullptr, false, true,
                              (int64_t)g.per_cu * rfr, false, rfr))
         return e;
